@@ -1,0 +1,96 @@
+"""Reusable activation scratch buffers and view-stripping helpers.
+
+(reference ``megatron/core/utils.py:24-124``).  On MI355X the caching
+allocator already recycles blocks cheaply, but gathering the full ``[s, b, h]``
+activation for sequence-parallel GEMMs in a named, persistent scratch tensor
+avoids allocator fragmentation across the 288 GB pool and keeps the address
+stable for hipGraph capture.
+"""
+import operator
+from functools import reduce
+
+import torch
+
+
+class GlobalMemoryBuffer:
+    """Named scratch tensors, grown on demand and handed out as views."""
+
+    def __init__(self):
+        self._buffers = {}
+
+    def get_tensor(self, shape, dtype, name):
+        numel = reduce(operator.mul, shape, 1)
+        key = (name, dtype)
+        buf = self._buffers.get(key)
+        if buf is None or buf.numel() < numel:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else "cpu"
+            buf = torch.empty(numel, dtype=dtype, device=device, requires_grad=False)
+            self._buffers[key] = buf
+        return buf[:numel].view(*shape)
+
+
+_GLOBAL_BUFFER = None
+
+
+def get_global_memory_buffer():
+    global _GLOBAL_BUFFER
+    if _GLOBAL_BUFFER is None:
+        _GLOBAL_BUFFER = GlobalMemoryBuffer()
+    return _GLOBAL_BUFFER
+
+
+def reset_global_memory_buffer():
+    global _GLOBAL_BUFFER
+    _GLOBAL_BUFFER = None
+
+
+def _kernel_make_viewless_tensor(inp, requires_grad):
+    out = torch.empty((1,), dtype=inp.dtype, device=inp.device, requires_grad=requires_grad)
+    out.data = inp.data
+    return out
+
+
+class MakeViewlessTensor(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, inp, requires_grad):
+        return _kernel_make_viewless_tensor(inp, requires_grad)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output, None
+
+
+def make_viewless_tensor(inp, requires_grad, keep_graph):
+    """Return a tensor sharing ``inp``'s storage whose ``._base`` is None, so
+    that pipeline "pseudo-free" of outputs actually releases memory."""
+    if inp._base is None:
+        return inp
+    if keep_graph:
+        return MakeViewlessTensor.apply(inp, requires_grad)
+    return _kernel_make_viewless_tensor(inp, requires_grad)
+
+
+def assert_viewless_tensor(tensor, extra_msg=None):
+    if isinstance(tensor, (list, tuple)):
+        for t in tensor:
+            assert_viewless_tensor(t, extra_msg)
+        return tensor
+    if not isinstance(tensor, torch.Tensor):
+        return tensor
+    if tensor._base is not None:
+        raise AssertionError("Ensure tensor._base is None before setting tensor.data or "
+                             f"storing tensor to memory buffer. Found tensor._base={tensor._base}. "
+                             f"{extra_msg or ''}")
+    return tensor
+
+
+def safely_set_viewless_tensor_data(tensor, new_data_tensor):
+    assert_viewless_tensor(tensor, extra_msg="FYI, tensor._base has shape "
+                           f"{'--' if tensor._base is None else tensor._base.shape}")
+    tensor.data = new_data_tensor
+
+
+def divide(numerator, denominator):
+    if numerator % denominator != 0:
+        raise AssertionError(f"{numerator} is not divisible by {denominator}")
+    return numerator // denominator

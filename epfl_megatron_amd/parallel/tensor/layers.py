@@ -1,0 +1,382 @@
+"""Tensor-parallel layers: column/row-parallel linear and vocab-parallel embedding.
+
+Weight shapes and attributes match the reference
+(``megatron/core/tensor_parallel/layers.py:128-701``): column-parallel
+weights are ``[out/tp, in]``, row-parallel ``[out, in/tp]``, row biases are
+not split.
+
+MI355X-specific design of the GEMM path (``_LinearFn``):
+
+* GEMMs run on hipBLASLt through ``torch.matmul``.
+* With ``gradient_accumulation_fusion`` the weight gradient is produced by a
+  bf16 x bf16 -> fp32 GEMM written **in place** into the fp32 ``main_grad``
+  view of the DDP bucket (beta = 1, ``torch.addmm(..., out_dtype=float32,
+  out=main_grad)``) — no separate wgrad tensor and no accumulate kernel
+  (reference N8 / apex ``fused_weight_gradient_mlp_cuda``).  Immediately after
+  enqueueing it we signal the DDP bucket manager, which can start that
+  bucket's RCCL reduction while backward continues (the reference only
+  reduces after the whole backward).
+* Under sequence parallelism the input all-gather for the wgrad is issued
+  before the dgrad GEMM and the dgrad reduce-scatter is overlapped with the
+  wgrad GEMM, using async RCCL work handles (RCCL runs on its own HIP stream;
+  ordering comes from events, not from ``CUDA_DEVICE_MAX_CONNECTIONS``).
+"""
+import math
+import warnings
+
+import torch
+import torch.nn.functional as F
+from torch.nn.parameter import Parameter
+
+from .. import state, comm
+from ..buffers import divide, get_global_memory_buffer
+from .mappings import (copy_to_tensor_model_parallel_region,
+                       gather_from_tensor_model_parallel_region,
+                       reduce_from_tensor_model_parallel_region,
+                       reduce_scatter_to_sequence_parallel_region,
+                       scatter_to_tensor_model_parallel_region)
+from .random import get_cuda_rng_tracker
+from .utils import VocabUtility
+
+_MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {
+    "tensor_model_parallel": False,
+    "partition_dim": -1,
+    "partition_stride": 1,
+}
+
+
+def param_is_not_tensor_parallel_duplicate(param):
+    return (getattr(param, "tensor_model_parallel", False)
+            or state.get_tensor_model_parallel_rank() == 0)
+
+
+def set_tensor_model_parallel_attributes(tensor, is_parallel, dim, stride):
+    for attr in _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS:
+        if hasattr(tensor, attr):
+            raise AssertionError(f"tensor already has attribute {attr}")
+    tensor.tensor_model_parallel = is_parallel
+    tensor.partition_dim = dim
+    tensor.partition_stride = stride
+
+
+def set_defaults_if_not_set_tensor_model_parallel_attributes(tensor):
+    for attr, val in _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS.items():
+        if not hasattr(tensor, attr):
+            setattr(tensor, attr, val)
+
+
+def copy_tensor_model_parallel_attributes(dst, src):
+    for attr in _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS:
+        if hasattr(src, attr):
+            setattr(dst, attr, getattr(src, attr))
+
+
+def _initialize_affine_weight_gpu(weight, init_method, partition_dim, stride=1):
+    set_tensor_model_parallel_attributes(weight, True, partition_dim, stride)
+    with get_cuda_rng_tracker().fork():
+        init_method(weight)
+
+
+def _initialize_affine_weight_cpu(weight, output_size, input_size, per_partition_size,
+                                  partition_dim, init_method, stride=1,
+                                  return_master_weight=False, params_dtype=torch.float32):
+    """Initialise the full master weight on CPU, then keep this rank's slice —
+    results are independent of the TP degree (used by --use_cpu_initialization)."""
+    set_tensor_model_parallel_attributes(weight, True, partition_dim, stride)
+    master = torch.empty(output_size, input_size, dtype=torch.float, requires_grad=False)
+    init_method(master)
+    master = master.to(dtype=params_dtype)
+    per_stride = divide(per_partition_size, stride)
+    pieces = torch.split(master, per_stride, dim=partition_dim)
+    rank = state.get_tensor_model_parallel_rank()
+    world = state.get_tensor_model_parallel_world_size()
+    mine = pieces[rank::world]
+    with torch.no_grad():
+        torch.cat(mine, dim=partition_dim, out=weight)
+    return master if return_master_weight else None
+
+
+def _default_device():
+    return torch.cuda.current_device() if torch.cuda.is_available() else "cpu"
+
+
+class VocabParallelEmbedding(torch.nn.Module):
+    """Embedding sharded along the vocab dim; out-of-shard ids contribute zeros
+    and the partial rows are summed with one TP all-reduce."""
+
+    def __init__(self, num_embeddings, embedding_dim, *, init_method=torch.nn.init.xavier_normal_,
+                 params_dtype=torch.float32, use_cpu_initialization=False,
+                 perform_initialization=True):
+        super().__init__()
+        self.num_embeddings = num_embeddings
+        self.embedding_dim = embedding_dim
+        self.tensor_model_parallel_size = state.get_tensor_model_parallel_world_size()
+        self.vocab_start_index, self.vocab_end_index = \
+            VocabUtility.vocab_range_from_global_vocab_size(
+                num_embeddings, state.get_tensor_model_parallel_rank(),
+                self.tensor_model_parallel_size)
+        self.num_embeddings_per_partition = self.vocab_end_index - self.vocab_start_index
+        if use_cpu_initialization or not torch.cuda.is_available():
+            self.weight = Parameter(torch.empty(self.num_embeddings_per_partition, embedding_dim,
+                                                dtype=params_dtype))
+            if perform_initialization:
+                _initialize_affine_weight_cpu(self.weight, num_embeddings, embedding_dim,
+                                              self.num_embeddings_per_partition, 0, init_method,
+                                              params_dtype=params_dtype)
+            else:
+                set_tensor_model_parallel_attributes(self.weight, True, 0, 1)
+        else:
+            self.weight = Parameter(torch.empty(self.num_embeddings_per_partition, embedding_dim,
+                                                device=_default_device(), dtype=params_dtype))
+            if perform_initialization:
+                _initialize_affine_weight_gpu(self.weight, init_method, partition_dim=0)
+            else:
+                set_tensor_model_parallel_attributes(self.weight, True, 0, 1)
+
+    def forward(self, input_):
+        if self.tensor_model_parallel_size > 1:
+            mask = (input_ < self.vocab_start_index) | (input_ >= self.vocab_end_index)
+            ids = input_.clone() - self.vocab_start_index
+            ids[mask] = 0
+        else:
+            ids = input_
+        out = F.embedding(ids, self.weight)
+        if self.tensor_model_parallel_size > 1:
+            out = out.masked_fill(mask.unsqueeze(-1), 0.0)
+        return reduce_from_tensor_model_parallel_region(out)
+
+
+def _notify_grad_ready(param):
+    cb = getattr(param, "_main_grad_ready", None)
+    if cb is not None:
+        cb()
+
+
+def _wgrad_into_main_grad(main_grad, grad_output_2d, input_2d):
+    """main_grad[out, in] += dY^T @ X with fp32 accumulation, in place."""
+    if main_grad.is_cuda and grad_output_2d.dtype in (torch.bfloat16, torch.float16):
+        torch.addmm(main_grad, grad_output_2d.t(), input_2d, out_dtype=torch.float32,
+                    out=main_grad)
+    else:
+        main_grad.addmm_(grad_output_2d.t().to(main_grad.dtype), input_2d.to(main_grad.dtype))
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input_, weight, bias, gradient_accumulation_fusion,
+                async_grad_allreduce, sequence_parallel):
+        ctx.save_for_backward(input_, weight)
+        ctx.use_bias = bias is not None
+        ctx.gradient_accumulation_fusion = gradient_accumulation_fusion
+        ctx.async_grad_allreduce = async_grad_allreduce
+        ctx.sequence_parallel = sequence_parallel
+        if sequence_parallel:
+            world = state.get_tensor_model_parallel_world_size()
+            shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
+            total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
+            comm.all_gather_into(total, input_, group=state.get_tensor_model_parallel_group())
+        else:
+            total = input_
+        out = torch.matmul(total, weight.t())
+        if bias is not None:
+            out = out + bias
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input_, weight = ctx.saved_tensors
+        tp_group = state.get_tensor_model_parallel_group() \
+            if state.get_tensor_model_parallel_world_size() > 1 else None
+        gather_handle = None
+        if ctx.sequence_parallel:
+            world = state.get_tensor_model_parallel_world_size()
+            shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
+            total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
+            gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
+        else:
+            total = input_
+        grad_input = grad_output.matmul(weight)
+        if gather_handle is not None:
+            gather_handle.wait()
+        go2 = grad_output.reshape(-1, grad_output.shape[-1])
+        ti2 = total.reshape(-1, total.shape[-1])
+        handle = None
+        if ctx.async_grad_allreduce and tp_group is not None:
+            handle = comm.all_reduce(grad_input, group=tp_group, async_op=True)
+        sub_grad_input = None
+        if ctx.sequence_parallel:
+            if ctx.async_grad_allreduce:
+                raise AssertionError("sequence parallel and async all-reduce are exclusive")
+            world = state.get_tensor_model_parallel_world_size()
+            sub_grad_input = torch.empty((input_.shape[0],) + tuple(input_.shape[1:]),
+                                         dtype=input_.dtype, device=input_.device)
+            handle = comm.reduce_scatter_into(sub_grad_input, grad_input, group=tp_group,
+                                              async_op=True)
+        if ctx.gradient_accumulation_fusion and hasattr(weight, "main_grad"):
+            _wgrad_into_main_grad(weight.main_grad, go2, ti2)
+            grad_weight = None
+            _notify_grad_ready(weight)
+        else:
+            grad_weight = go2.t().matmul(ti2)
+        grad_bias = go2.sum(dim=0) if ctx.use_bias else None
+        if ctx.sequence_parallel:
+            if handle is not None:
+                handle.wait()
+            return sub_grad_input, grad_weight, grad_bias, None, None, None
+        if handle is not None:
+            handle.wait()
+        return grad_input, grad_weight, grad_bias, None, None, None
+
+
+def linear_with_grad_accumulation_and_async_allreduce(input, weight, bias,
+                                                      gradient_accumulation_fusion,
+                                                      async_grad_allreduce,
+                                                      sequence_parallel_enabled):
+    return _LinearFn.apply(input, weight, bias, gradient_accumulation_fusion,
+                           async_grad_allreduce, sequence_parallel_enabled)
+
+
+def _make_weight(rows, cols, dtype, use_cpu_init):
+    if use_cpu_init or not torch.cuda.is_available():
+        return Parameter(torch.empty(rows, cols, dtype=dtype))
+    return Parameter(torch.empty(rows, cols, device=_default_device(), dtype=dtype))
+
+
+def _make_bias(n, dtype, use_cpu_init):
+    if use_cpu_init or not torch.cuda.is_available():
+        b = Parameter(torch.empty(n, dtype=dtype))
+    else:
+        b = Parameter(torch.empty(n, device=_default_device(), dtype=dtype))
+    with torch.no_grad():
+        b.zero_()
+    return b
+
+
+class ColumnParallelLinear(torch.nn.Module):
+    """Y = XA + b with A split along its output dim: A = [A_1 ... A_p]."""
+
+    def __init__(self, input_size, output_size, *, bias=True, gather_output=True,
+                 init_method=torch.nn.init.xavier_normal_, stride=1, keep_master_weight_for_test=False,
+                 skip_bias_add=False, async_tensor_model_parallel_allreduce=True,
+                 params_dtype=torch.float32, use_cpu_initialization=False,
+                 perform_initialization=True, gradient_accumulation_fusion=False,
+                 sequence_parallel_enabled=False):
+        super().__init__()
+        self.input_size = input_size
+        self.output_size = output_size
+        self.gather_output = gather_output
+        world = state.get_tensor_model_parallel_world_size()
+        self.output_size_per_partition = divide(output_size, world)
+        self.skip_bias_add = skip_bias_add
+        self.weight = _make_weight(self.output_size_per_partition, input_size, params_dtype,
+                                   use_cpu_initialization)
+        if perform_initialization:
+            if use_cpu_initialization or not torch.cuda.is_available():
+                self.master_weight = _initialize_affine_weight_cpu(
+                    self.weight, output_size, input_size, self.output_size_per_partition, 0,
+                    init_method, stride=stride, return_master_weight=keep_master_weight_for_test,
+                    params_dtype=params_dtype)
+            else:
+                _initialize_affine_weight_gpu(self.weight, init_method, partition_dim=0,
+                                              stride=stride)
+        else:
+            set_tensor_model_parallel_attributes(self.weight, True, 0, stride)
+        if bias:
+            self.bias = _make_bias(self.output_size_per_partition, params_dtype,
+                                   use_cpu_initialization)
+            set_tensor_model_parallel_attributes(self.bias, True, 0, stride)
+        else:
+            self.register_parameter("bias", None)
+        self.async_tensor_model_parallel_allreduce = (
+            async_tensor_model_parallel_allreduce and world > 1)
+        if sequence_parallel_enabled and world <= 1:
+            warnings.warn("`sequence_parallel_enabled` is set to `True`, but tensor model "
+                          "parallel size is 1; disabling it.")
+            sequence_parallel_enabled = False
+        self.sequence_parallel_enabled = sequence_parallel_enabled
+        self.gradient_accumulation_fusion = gradient_accumulation_fusion
+        if self.async_tensor_model_parallel_allreduce and self.sequence_parallel_enabled:
+            raise RuntimeError("`async_tensor_model_parallel_allreduce` and "
+                               "`sequence_parallel_enabled` cannot be enabled at the same time.")
+
+    def forward(self, input_):
+        bias = self.bias if not self.skip_bias_add else None
+        if self.async_tensor_model_parallel_allreduce or self.sequence_parallel_enabled:
+            input_parallel = input_
+        else:
+            input_parallel = copy_to_tensor_model_parallel_region(input_)
+        output_parallel = _LinearFn.apply(input_parallel, self.weight, bias,
+                                          self.gradient_accumulation_fusion,
+                                          self.async_tensor_model_parallel_allreduce,
+                                          self.sequence_parallel_enabled)
+        if self.gather_output:
+            if self.sequence_parallel_enabled:
+                raise AssertionError("gather_output is incompatible with sequence parallelism")
+            output = gather_from_tensor_model_parallel_region(output_parallel)
+        else:
+            output = output_parallel
+        output_bias = self.bias if self.skip_bias_add else None
+        return output, output_bias
+
+
+class RowParallelLinear(torch.nn.Module):
+    """Y = XA + b with A split along its input dim; partial outputs are summed
+    with an all-reduce (or reduce-scattered along the sequence under SP)."""
+
+    def __init__(self, input_size, output_size, *, bias=True, input_is_parallel=False,
+                 init_method=torch.nn.init.xavier_normal_, stride=1,
+                 keep_master_weight_for_test=False, skip_bias_add=False,
+                 params_dtype=torch.float32, use_cpu_initialization=False,
+                 perform_initialization=True, gradient_accumulation_fusion=False,
+                 sequence_parallel_enabled=False):
+        super().__init__()
+        self.input_size = input_size
+        self.output_size = output_size
+        self.input_is_parallel = input_is_parallel
+        world = state.get_tensor_model_parallel_world_size()
+        self.input_size_per_partition = divide(input_size, world)
+        self.skip_bias_add = skip_bias_add
+        self.gradient_accumulation_fusion = gradient_accumulation_fusion
+        self.sequence_parallel_enabled = sequence_parallel_enabled
+        if self.sequence_parallel_enabled and not self.input_is_parallel:
+            raise RuntimeError("To enable `sequence_parallel_enabled`, `input_is_parallel` "
+                               "must be `True`")
+        self.weight = _make_weight(output_size, self.input_size_per_partition, params_dtype,
+                                   use_cpu_initialization)
+        if perform_initialization:
+            if use_cpu_initialization or not torch.cuda.is_available():
+                self.master_weight = _initialize_affine_weight_cpu(
+                    self.weight, output_size, input_size, self.input_size_per_partition, 1,
+                    init_method, stride=stride, return_master_weight=keep_master_weight_for_test,
+                    params_dtype=params_dtype)
+            else:
+                _initialize_affine_weight_gpu(self.weight, init_method, partition_dim=1,
+                                              stride=stride)
+        else:
+            set_tensor_model_parallel_attributes(self.weight, True, 1, stride)
+        if bias:
+            self.bias = _make_bias(output_size, params_dtype, use_cpu_initialization)
+            setattr(self.bias, "sequence_parallel", sequence_parallel_enabled)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, input_):
+        if self.input_is_parallel:
+            input_parallel = input_
+        else:
+            if self.sequence_parallel_enabled:
+                raise AssertionError("sequence parallelism needs a parallel input")
+            input_parallel = scatter_to_tensor_model_parallel_region(input_)
+        output_parallel = _LinearFn.apply(input_parallel, self.weight, None,
+                                          self.gradient_accumulation_fusion, False, False)
+        if self.sequence_parallel_enabled:
+            output_ = reduce_scatter_to_sequence_parallel_region(output_parallel)
+        else:
+            output_ = reduce_from_tensor_model_parallel_region(output_parallel)
+        if not self.skip_bias_add:
+            output = output_ + self.bias if self.bias is not None else output_
+            output_bias = None
+        else:
+            output = output_
+            output_bias = self.bias
+        return output, output_bias
