@@ -1,0 +1,120 @@
+"""Ahead-of-time build of the native extensions (no JIT, no hipify).
+
+* ``epfl_megatron_amd/_C.so``  — gfx950 HIP kernels (``csrc/*.hip``, compiled by
+  ``hipcc --offload-arch=gfx950``) + pybind11/ATen bindings (``csrc/bindings.cpp``).
+* ``epfl_megatron_amd/data/_helpers.so`` — CPU dataset index builders
+  (``csrc/data_helpers.cpp``, g++ + pybind11).
+
+Both land in-tree so they travel with the repository snapshot to the GPU box.
+Usage: ``python -m epfl_megatron_amd.build [--force] [--jobs N]``.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(os.path.dirname(PKG), "build", "csrc")
+ARCH = os.environ.get("EMA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch
+    import torch.utils.cpp_extension as ce
+    inc = ce.include_paths()
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build_kernels(force=False, jobs=None):
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    inc, lib, abi = _torch_paths()
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
+              "-mcode-object-version=5", "-Wno-unused-result"]
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            jobs_list.append([HIPCC, "-c", src, "-o", obj] + common)
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(BUILD, "bindings.cpp.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [bsrc] + headers):
+        cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-O2", "-std=c++17", "-fPIC", "-I", CSRC,
+               f"--offload-arch={ARCH}",
+               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
+               "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+               "-I", sysconfig.get_paths()["include"], "-Wno-unused-result",
+               "-Wno-deprecated-declarations"]
+        for i in inc:
+            cmd += ["-I", i]
+        jobs_list.append(cmd)
+    n = jobs or int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(n, 16))) as ex:
+        list(ex.map(_run, jobs_list))
+    out = os.path.join(PKG, "_C.so")
+    if force or jobs_list or not os.path.exists(out):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs +
+             ["-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+              "-ltorch_python", f"-Wl,-rpath,{lib}"])
+    return out
+
+
+def build_data_helpers(force=False):
+    import pybind11
+    src = os.path.join(CSRC, "data_helpers.cpp")
+    out = os.path.join(PKG, "data", "_helpers.so")
+    if not os.path.exists(src):
+        return None
+    if force or _newer(out, [src]):
+        _run(["g++", "-O3", "-shared", "-std=c++17", "-fPIC", "-I", pybind11.get_include(),
+              "-I", sysconfig.get_paths()["include"], src, "-o", out])
+    return out
+
+
+def build_all(force=False, jobs=None):
+    h = build_data_helpers(force)
+    k = build_kernels(force, jobs)
+    return k, h
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--only", choices=["kernels", "data"], default=None)
+    a = ap.parse_args()
+    if a.only == "data":
+        print(build_data_helpers(a.force))
+    elif a.only == "kernels":
+        print(build_kernels(a.force, a.jobs))
+    else:
+        print(build_all(a.force, a.jobs))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

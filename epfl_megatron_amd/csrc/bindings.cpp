@@ -1,0 +1,478 @@
+// Python bindings for the gfx950 kernels (module epfl_megatron_amd._C).
+//
+// Every op launches on PyTorch's current HIP stream (c10::hip), allocates
+// outputs/workspaces through the caching allocator, validates shapes/dtypes
+// on the host BEFORE launching (a mis-shaped launch on a shared MI355X node
+// can fault the whole machine), and never synchronises.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtype_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ema::DT_F32;
+    case at::kHalf: return ema::DT_F16;
+    case at::kBFloat16: return ema::DT_BF16;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void check_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+
+void check_vec_aligned(const at::Tensor& t, const char* name) {
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name,
+              " must be 16-byte aligned");
+}
+
+at::Tensor as_dtype(const at::Tensor& w, const at::Tensor& like) {
+  return w.scalar_type() == like.scalar_type() ? w.contiguous() : w.to(like.scalar_type()).contiguous();
+}
+
+// ---------------------------------------------------------------- norms
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [rows, H]");
+  const int64_t rows = x.size(0);
+  const int H = (int)x.size(1);
+  const int dt = dtype_code(x);
+  TORCH_CHECK(H % (16 / x.element_size()) == 0, "hidden size must be a multiple of 16 bytes");
+  TORCH_CHECK(H <= ema::norm_max_hidden(dt), "hidden size too large for the norm kernel");
+  TORCH_CHECK(w.numel() == H, "weight size mismatch");
+  check_vec_aligned(x, "x");
+  auto wc = as_dtype(w, x);
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  if (rows > 0)
+    ema::rmsnorm_fwd(x.data_ptr(), wc.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), rows, H,
+                     (float)eps, dt, cur_stream());
+  return {y, rstd};
+}
+
+std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                    const at::Tensor& rstd) {
+  check_gpu(x, "x");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
+  const int64_t rows = x.size(0);
+  const int H = (int)x.size(1);
+  const int dt = dtype_code(x);
+  auto wc = as_dtype(w, x);
+  auto dx = at::empty_like(x);
+  auto dw = at::empty({H}, x.options());
+  const int P = ema::norm_bwd_partials(rows);
+  auto part = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
+  if (rows > 0) {
+    ema::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), rstd.data_ptr<float>(),
+                     dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), rows, H, dt,
+                     cur_stream());
+  } else {
+    dw.zero_();
+  }
+  return {dx, dw.to(w.scalar_type())};
+}
+
+std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w,
+                                      const c10::optional<at::Tensor>& b, double eps) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [rows, H]");
+  const int64_t rows = x.size(0);
+  const int H = (int)x.size(1);
+  const int dt = dtype_code(x);
+  TORCH_CHECK(H % (16 / x.element_size()) == 0, "hidden size must be a multiple of 16 bytes");
+  TORCH_CHECK(H <= ema::norm_max_hidden(dt), "hidden size too large for the norm kernel");
+  TORCH_CHECK(w.numel() == H, "weight size mismatch");
+  auto wc = as_dtype(w, x);
+  at::Tensor bc;
+  if (b.has_value() && b->defined()) bc = as_dtype(*b, x);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  if (rows > 0)
+    ema::layernorm_fwd(x.data_ptr(), wc.data_ptr(), bc.defined() ? bc.data_ptr() : nullptr,
+                       y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H,
+                       (float)eps, dt, cur_stream());
+  return {y, mean, rstd};
+}
+
+std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
+                                      const at::Tensor& w, const at::Tensor& mean,
+                                      const at::Tensor& rstd) {
+  check_gpu(x, "x");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
+  const int64_t rows = x.size(0);
+  const int H = (int)x.size(1);
+  const int dt = dtype_code(x);
+  auto wc = as_dtype(w, x);
+  auto dx = at::empty_like(x);
+  auto dw = at::empty({H}, x.options());
+  auto db = at::empty({H}, x.options());
+  const int P = ema::norm_bwd_partials(rows);
+  auto pw = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
+  auto pb = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
+  if (rows > 0) {
+    ema::layernorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), mean.data_ptr<float>(),
+                       rstd.data_ptr<float>(), dx.data_ptr(), pw.data_ptr<float>(),
+                       pb.data_ptr<float>(), dw.data_ptr(), db.data_ptr(), rows, H, dt,
+                       cur_stream());
+  } else {
+    dw.zero_();
+    db.zero_();
+  }
+  return {dx, dw.to(w.scalar_type()), db.to(w.scalar_type())};
+}
+
+// ---------------------------------------------------------------- rope
+void rope_qkv_inplace(at::Tensor qkv5, const at::Tensor& cos, const at::Tensor& sin,
+                      const c10::optional<at::Tensor>& pos, int64_t offset, bool inverse) {
+  check_gpu(qkv5, "qkv");
+  TORCH_CHECK(qkv5.dim() == 5, "qkv must be [s, b, ng, r+2, hd]");
+  TORCH_CHECK(qkv5.stride(4) == 1, "head_dim must be contiguous");
+  const int S = (int)qkv5.size(0), B = (int)qkv5.size(1), G = (int)qkv5.size(2);
+  const int R = (int)qkv5.size(3) - 2, HD = (int)qkv5.size(4);
+  TORCH_CHECK(HD % 8 == 0, "head_dim must be a multiple of 8");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous(),
+              "rope tables must be contiguous fp32");
+  TORCH_CHECK(cos.size(1) == HD / 2, "rope table width must be head_dim / 2");
+  TORCH_CHECK((qkv5.stride(3) % 8) == 0 && (qkv5.stride(2) % 8) == 0 && (qkv5.stride(1) % 8) == 0 &&
+              (qkv5.stride(0) % 8) == 0, "qkv strides must keep 16-byte alignment");
+  const int64_t max_pos = cos.size(0);
+  const int64_t* pp = nullptr;
+  int64_t psb = 0;
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->dim() == 2 && pos->size(0) == B &&
+                pos->size(1) == S, "position_ids must be int64 [b, s]");
+    TORCH_CHECK(pos->stride(1) == 1, "position_ids rows must be contiguous");
+    pp = pos->data_ptr<int64_t>();
+    psb = pos->stride(0);
+  } else {
+    TORCH_CHECK(offset + S <= max_pos, "rope table too short for sequence");
+  }
+  ema::rope_qkv_inplace(qkv5.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pp, psb,
+                        S, B, G, R, HD, qkv5.stride(0), qkv5.stride(1), qkv5.stride(2),
+                        qkv5.stride(3), (int)offset, inverse ? 1 : 0, dtype_code(qkv5),
+                        cur_stream());
+}
+
+// ---------------------------------------------------------------- activations
+at::Tensor glu_fwd(const at::Tensor& x, int64_t kind) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+  const int64_t two_f = x.size(-1);
+  TORCH_CHECK(two_f % 2 == 0, "GLU input width must be even");
+  const int F = (int)(two_f / 2);
+  TORCH_CHECK(F % (16 / x.element_size()) == 0, "GLU width must be a multiple of 16 bytes");
+  const int64_t rows = x.numel() / two_f;
+  auto sizes = x.sizes().vec();
+  sizes.back() = F;
+  auto y = at::empty(sizes, x.options());
+  if (rows > 0) ema::glu_fwd(x.data_ptr(), y.data_ptr(), rows, F, (int)kind, dtype_code(x), cur_stream());
+  return y;
+}
+
+at::Tensor glu_bwd(const at::Tensor& dy, const at::Tensor& x, int64_t kind) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous(), "inputs must be contiguous");
+  const int64_t two_f = x.size(-1);
+  const int F = (int)(two_f / 2);
+  const int64_t rows = x.numel() / two_f;
+  TORCH_CHECK(dy.numel() == rows * F, "dy shape mismatch");
+  auto dx = at::empty_like(x);
+  if (rows > 0)
+    ema::glu_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), rows, F, (int)kind, dtype_code(x),
+                 cur_stream());
+  return dx;
+}
+
+at::Tensor gelu_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& bias, int64_t approx) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+  const int F = (int)x.size(-1);
+  TORCH_CHECK(F % (16 / x.element_size()) == 0, "width must be a multiple of 16 bytes");
+  const int64_t rows = x.numel() / F;
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = as_dtype(*bias, x);
+    TORCH_CHECK(b.numel() == F, "bias size mismatch");
+  }
+  auto y = at::empty_like(x);
+  if (rows > 0)
+    ema::gelu_fwd(x.data_ptr(), b.defined() ? b.data_ptr() : nullptr, y.data_ptr(), rows, F,
+                  (int)approx, dtype_code(x), cur_stream());
+  return y;
+}
+
+at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& bias,
+                    int64_t approx) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
+  const int F = (int)x.size(-1);
+  const int64_t rows = x.numel() / F;
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) b = as_dtype(*bias, x);
+  auto dx = at::empty_like(x);
+  if (rows > 0)
+    ema::gelu_bwd(dy.data_ptr(), x.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
+                  dx.data_ptr(), rows, F, (int)approx, dtype_code(x), cur_stream());
+  return dx;
+}
+
+// ---------------------------------------------------------------- cross entropy
+void check_ce(const at::Tensor& z, const at::Tensor& t) {
+  check_gpu(z, "logits");
+  TORCH_CHECK(z.dim() == 2 && z.is_contiguous(), "logits must be contiguous [rows, V]");
+  TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous() && t.numel() == z.size(0),
+              "target must be int64 [rows]");
+  TORCH_CHECK(z.size(1) % (16 / z.element_size()) == 0, "vocab shard must be a multiple of 16 bytes");
+  check_vec_aligned(z, "logits");
+}
+
+std::vector<at::Tensor> ce_fwd_fused(const at::Tensor& z, const at::Tensor& t) {
+  check_ce(z, t);
+  const int64_t rows = z.size(0);
+  auto loss = at::empty({rows}, z.options().dtype(at::kFloat));
+  auto lse = at::empty({rows}, z.options().dtype(at::kFloat));
+  if (rows > 0)
+    ema::ce_fwd_fused(z.data_ptr(), t.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                      lse.data_ptr<float>(), rows, (int)z.size(1), dtype_code(z), cur_stream());
+  return {loss, lse};
+}
+
+at::Tensor ce_row_max(const at::Tensor& z) {
+  check_gpu(z, "logits");
+  TORCH_CHECK(z.dim() == 2 && z.is_contiguous(), "logits must be contiguous [rows, V]");
+  const int64_t rows = z.size(0);
+  auto m = at::empty({rows}, z.options().dtype(at::kFloat));
+  if (rows > 0) ema::ce_row_max(z.data_ptr(), m.data_ptr<float>(), rows, (int)z.size(1), dtype_code(z), cur_stream());
+  return m;
+}
+
+std::vector<at::Tensor> ce_sumexp_target(const at::Tensor& z, const at::Tensor& t,
+                                         const at::Tensor& rmax, int64_t vstart) {
+  check_ce(z, t);
+  const int64_t rows = z.size(0);
+  auto se = at::empty({rows}, z.options().dtype(at::kFloat));
+  auto tl = at::empty({rows}, z.options().dtype(at::kFloat));
+  if (rows > 0)
+    ema::ce_sumexp_target(z.data_ptr(), t.data_ptr<int64_t>(), rmax.data_ptr<float>(),
+                          se.data_ptr<float>(), tl.data_ptr<float>(), rows, (int)z.size(1), vstart,
+                          dtype_code(z), cur_stream());
+  return {se, tl};
+}
+
+at::Tensor ce_bwd(const at::Tensor& z, const at::Tensor& t, const at::Tensor& lse,
+                  const at::Tensor& dl, int64_t vstart) {
+  check_ce(z, t);
+  TORCH_CHECK(lse.numel() == z.size(0) && dl.numel() == z.size(0) && dl.scalar_type() == at::kFloat,
+              "lse / dloss must be fp32 [rows]");
+  auto dz = at::empty_like(z);
+  const int64_t rows = z.size(0);
+  if (rows > 0)
+    ema::ce_bwd(z.data_ptr(), t.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                dl.contiguous().data_ptr<float>(), dz.data_ptr(), rows, (int)z.size(1), vstart,
+                dtype_code(z), cur_stream());
+  return dz;
+}
+
+// ---------------------------------------------------------------- softmax
+at::Tensor softmax_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& mask, double scale,
+                       int64_t mode) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "scores must be contiguous [b, np, sq, sk]");
+  const int64_t B = x.size(0), NP = x.size(1);
+  const int SQ = (int)x.size(2), SK = (int)x.size(3);
+  TORCH_CHECK(SK <= 8192, "sk must be <= 8192");
+  if (mode == 1) TORCH_CHECK(SQ == SK, "causal softmax expects square scores");
+  const uint8_t* mp = nullptr;
+  at::Tensor m;
+  if (mode == 2) {
+    TORCH_CHECK(mask.has_value() && mask->defined(), "mask required for mode 2");
+    m = mask->to(at::kByte).contiguous();
+    TORCH_CHECK(m.dim() == 4 && m.size(0) == B && m.size(1) == 1 && m.size(2) == SQ && m.size(3) == SK,
+                "mask must be [b, 1, sq, sk]");
+    mp = m.data_ptr<uint8_t>();
+  }
+  auto y = at::empty_like(x);
+  if (x.numel() > 0)
+    ema::softmax_fwd(x.data_ptr(), mp, y.data_ptr(), B, NP, SQ, SK, (float)scale, (int)mode,
+                     dtype_code(x), cur_stream());
+  return y;
+}
+
+at::Tensor softmax_bwd(const at::Tensor& dy, const at::Tensor& y, double scale) {
+  check_gpu(y, "y");
+  TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dy.sizes() == y.sizes(), "shape mismatch");
+  const int SK = (int)y.size(-1);
+  const int64_t rows = y.numel() / SK;
+  auto dx = at::empty_like(y);
+  if (rows > 0) ema::softmax_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), rows, SK, (float)scale, dtype_code(y), cur_stream());
+  return dx;
+}
+
+// ---------------------------------------------------------------- optimizer
+void check_table(const at::Tensor& table) {
+  check_gpu(table, "table");
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 4 &&
+              table.is_contiguous(), "chunk table must be int64 [n, 4]");
+}
+
+at::Tensor chunked_sumsq(const at::Tensor& grad, const at::Tensor& table) {
+  check_gpu(grad, "grad");
+  check_table(table);
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous(), "grad must be fp32 flat");
+  check_vec_aligned(grad, "grad");
+  const int n = (int)table.size(0);
+  auto part = at::empty({n}, grad.options());
+  auto out = at::empty({}, grad.options());
+  ema::chunked_sumsq(grad.data_ptr<float>(), table.data_ptr<int64_t>(), n, part.data_ptr<float>(),
+                     out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+void flat_adam(at::Tensor master, const c10::optional<at::Tensor>& model_out, const at::Tensor& grad,
+               at::Tensor m, at::Tensor v, const at::Tensor& table, std::vector<double> lrs,
+               std::vector<double> wds, double beta1, double beta2, double eps, double bc1,
+               double bc2, double grad_scale, bool adam_w_mode) {
+  check_gpu(master, "master");
+  check_table(table);
+  for (const at::Tensor* t : {&master, &m, &v}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "fp32 flat state expected");
+    TORCH_CHECK(t->numel() == master.numel(), "state size mismatch");
+    check_vec_aligned(*t, "state");
+  }
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous(), "grad must be fp32 flat");
+  check_vec_aligned(grad, "grad");
+  TORCH_CHECK(lrs.size() == wds.size() && lrs.size() <= 8, "at most 8 param groups");
+  ema::AdamArgs a{};
+  for (size_t i = 0; i < lrs.size(); ++i) {
+    a.lr[i] = (float)lrs[i];
+    a.wd[i] = (float)wds[i];
+  }
+  a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.bc1 = (float)bc1; a.bc2 = (float)bc2; a.grad_scale = (float)grad_scale;
+  a.adam_w_mode = adam_w_mode ? 1 : 0;
+  void* mo = nullptr;
+  int mdt = ema::DT_F32;
+  if (model_out.has_value() && model_out->defined()) {
+    TORCH_CHECK(model_out->is_contiguous() && model_out->numel() == grad.numel(),
+                "model buffer must match the grad buffer layout");
+    check_vec_aligned(*model_out, "model params");
+    mo = model_out->data_ptr();
+    mdt = dtype_code(*model_out);
+  }
+  ema::flat_adam(master.data_ptr<float>(), mo, mdt, grad.data_ptr<float>(), m.data_ptr<float>(),
+                 v.data_ptr<float>(), table.data_ptr<int64_t>(), (int)table.size(0), a, cur_stream());
+}
+
+// ---------------------------------------------------------------- attention
+ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                          const at::Tensor& out, const at::Tensor& lse, int64_t b, int64_t sq,
+                          int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
+                          const std::vector<int64_t>& qs, const std::vector<int64_t>& ks,
+                          const std::vector<int64_t>& vs, const std::vector<int64_t>& os,
+                          bool causal, double scale) {
+  TORCH_CHECK(qs.size() == 4 && ks.size() == 3 && vs.size() == 3 && os.size() == 3, "bad strides");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type() &&
+              q.scalar_type() == out.scalar_type(), "q/k/v/out dtype mismatch");
+  TORCH_CHECK(ema::flash_attn_supported((int)hd, dtype_code(q)), "flash attention supports bf16/fp16 "
+              "with head_dim 64 or 128 (got ", hd, ")");
+  TORCH_CHECK(nkv > 0 && nq % nkv == 0, "nq must be a multiple of nkv");
+  TORCH_CHECK(sq > 0 && sk > 0 && b > 0, "empty attention");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == b * nq * sq && lse.is_contiguous(),
+              "lse must be fp32 [b, nq, sq]");
+  for (int64_t s : qs) TORCH_CHECK(s % 8 == 0, "q strides must keep 16-byte alignment");
+  for (int64_t s : ks) TORCH_CHECK(s % 8 == 0, "k strides must keep 16-byte alignment");
+  for (int64_t s : vs) TORCH_CHECK(s % 8 == 0, "v strides must keep 16-byte alignment");
+  for (int64_t s : os) TORCH_CHECK(s % 4 == 0, "o strides must keep 8-byte alignment");
+  for (const at::Tensor* t : {&q, &k, &v}) check_vec_aligned(*t, "q/k/v");
+  // Every address the kernel can form must lie inside its tensor's storage.
+  auto span = [](int64_t b, int64_t s, int64_t n, int64_t sb, int64_t ss, int64_t sn, int64_t hd) {
+    return (b - 1) * sb + (s - 1) * ss + (n - 1) * sn + hd;
+  };
+  const int64_t r = nq / nkv;
+  const int64_t qspan = (b - 1) * qs[0] + (sq - 1) * qs[1] + (nkv - 1) * qs[2] + (r - 1) * qs[3] + hd;
+  TORCH_CHECK(q.storage_offset() + qspan <= (int64_t)(q.storage().nbytes() / q.element_size()),
+              "q strides exceed storage");
+  TORCH_CHECK(k.storage_offset() + span(b, sk, nkv, ks[0], ks[1], ks[2], hd) <=
+              (int64_t)(k.storage().nbytes() / k.element_size()), "k strides exceed storage");
+  TORCH_CHECK(v.storage_offset() + span(b, sk, nkv, vs[0], vs[1], vs[2], hd) <=
+              (int64_t)(v.storage().nbytes() / v.element_size()), "v strides exceed storage");
+  TORCH_CHECK(out.storage_offset() + span(b, sq, nq, os[0], os[1], os[2], hd) <=
+              (int64_t)(out.storage().nbytes() / out.element_size()), "out strides exceed storage");
+  ema::AttnParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = out.data_ptr();
+  p.lse = lse.data_ptr<float>();
+  p.b = (int)b; p.sq = (int)sq; p.sk = (int)sk; p.nq = (int)nq; p.nkv = (int)nkv; p.hd = (int)hd;
+  p.q_sb = qs[0]; p.q_ss = qs[1]; p.q_sg = qs[2]; p.q_sh = qs[3];
+  p.k_sb = ks[0]; p.k_ss = ks[1]; p.k_sg = ks[2];
+  p.v_sb = vs[0]; p.v_ss = vs[1]; p.v_sg = vs[2];
+  p.o_sb = os[0]; p.o_ss = os[1]; p.o_sh = os[2];
+  p.causal = causal ? 1 : 0;
+  p.scale = (float)scale;
+  return p;
+}
+
+void flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
+                    at::Tensor lse, int64_t b, int64_t sq, int64_t sk, int64_t nq, int64_t nkv,
+                    int64_t hd, std::vector<int64_t> qs, std::vector<int64_t> ks,
+                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale) {
+  check_gpu(q, "q");
+  auto p = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
+}
+
+void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                    const at::Tensor& v, const at::Tensor& out, const at::Tensor& lse, at::Tensor dq,
+                    at::Tensor dk, at::Tensor dv, int64_t b, int64_t sq, int64_t sk, int64_t nq,
+                    int64_t nkv, int64_t hd, std::vector<int64_t> qs, std::vector<int64_t> ks,
+                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale) {
+  check_gpu(q, "q");
+  auto f = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  TORCH_CHECK(dout.scalar_type() == q.scalar_type(), "dout dtype mismatch");
+  TORCH_CHECK(dout.stride(-1) == 1, "dout head_dim must be contiguous");
+  ema::AttnBwdParams p{};
+  p.f = f;
+  p.dout = dout.data_ptr();
+  p.dq = dq.data_ptr();
+  p.dk = dk.data_ptr();
+  p.dv = dv.data_ptr();
+  auto dq_acc = at::empty({b * nq * sq * hd}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({b * nq * sq}, q.options().dtype(at::kFloat));
+  p.dq_acc = dq_acc.data_ptr<float>();
+  p.delta = delta.data_ptr<float>();
+  ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"));
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rope_qkv_inplace", &rope_qkv_inplace);
+  m.def("glu_fwd", &glu_fwd);
+  m.def("glu_bwd", &glu_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("ce_fwd_fused", &ce_fwd_fused);
+  m.def("ce_row_max", &ce_row_max);
+  m.def("ce_sumexp_target", &ce_sumexp_target);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("softmax_fwd", &softmax_fwd);
+  m.def("softmax_bwd", &softmax_bwd);
+  m.def("chunked_sumsq", &chunked_sumsq);
+  m.def("flat_adam", &flat_adam);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+}

@@ -1,0 +1,89 @@
+// Shared pieces of the gfx950 FlashAttention-2 forward/backward kernels.
+//
+// MFMA: v_mfma_f32_32x32x16_{bf16,f16}.  Fragment maps (CDNA guide §3):
+//   A[row = lane&31][k = 8*(lane>>5) + j],  B[k = 8*(lane>>5) + j][col = lane&31]
+//   C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5), reg = 0..15.
+// An accumulator used as the next MFMA's B operand: registers 8s..8s+7 form
+// k-step s with k = 16s + 8(j>>2) + 4h + (j&3) (j = element, h = lane>>5).
+#pragma once
+#include "common.h"
+
+namespace ema {
+namespace fa {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
+template <typename T>
+struct MT;
+template <>
+struct MT<bf16> {
+  typedef bf16x8 x8;
+  typedef bf16x4 x4;
+  static __device__ __forceinline__ f32x16 mfma(x8 a, x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ x4 tr_read(const bf16* lds) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) x4*)(lds));
+  }
+};
+template <>
+struct MT<fp16> {
+  typedef f16x8 x8;
+  typedef f16x4 x4;
+  static __device__ __forceinline__ f32x16 mfma(x8 a, x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ x4 tr_read(const fp16* lds) {
+    typedef __attribute__((ext_vector_type(4))) short s4;
+    const s4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s4*)(lds));
+    return __builtin_bit_cast(x4, r);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x8 ld8(const T* p) {
+  return *reinterpret_cast<const typename MT<T>::x8*>(p);
+}
+
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x8 join(typename MT<T>::x4 a, typename MT<T>::x4 b) {
+  typename MT<T>::x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// Registers 8s..8s+7 of an fp32 accumulator -> operand fragment of k-step s.
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x8 acc_frag(const f32x16& acc, int s) {
+  typename MT<T>::x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (T)acc[8 * s + j];
+  return r;
+}
+
+__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// 16-byte-chunk XOR swizzle for [rows][HD] tiles that are read both by rows
+// (ds_read_b128 A/B fragments) and transposed (ds_read_b64_tr_b16): CDNA guide
+// T10 image (b) for 256-byte rows; a 3-bit analogue for 128-byte rows.
+template <int HD>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (HD == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return ((row & 3) << 1) | ((row >> 2) & 1);
+}
+
+// Element offset of (row, col) in a swizzled [rows][HD] tile (col multiple of 4).
+template <int HD>
+__device__ __forceinline__ int sw_off(int row, int col) {
+  return row * HD + (((col >> 3) ^ swz<HD>(row)) << 3) + (col & 7);
+}
+
+}  // namespace fa
+}  // namespace ema

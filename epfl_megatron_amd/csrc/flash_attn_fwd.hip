@@ -1,0 +1,231 @@
+// FlashAttention-2 forward for gfx950 (MI355X), native GQA/MQA, causal.
+//
+// Workgroup = 4 waves = a 128-row query block of one (batch, query head);
+// each wave owns 32 query rows.  K/V tiles of 64 keys stream through LDS
+// (register-staged: the next tile's global loads are issued before the current
+// tile's MFMAs and written to LDS after them, CDNA guide T14).
+//
+// Per 32(q) x 64(k) step a wave runs 2 x HD/16 MFMAs for S^T = K Q^T and
+// 2 x 2 x HD/32 MFMAs for O^T += V^T P^T (v_mfma_f32_32x32x16).  S is computed
+// transposed ("swapped QK^T", guide T12) so a query row lives on one lane pair
+// (lane, lane^32): the online-softmax max/sum is 31 in-register ops + one
+// cross-half shuffle, the O rescale is a per-lane scalar, and the P
+// accumulator feeds the PV MFMA as its B operand with no LDS round trip.  V is
+// read from LDS with ds_read_b64_tr_b16 (hardware transpose, guide T10) from a
+// row-padded image (conflict-free); K uses an XOR-swizzled image (T2).
+//
+// Query head j reads KV group j / (nq / nkv) directly (no K/V expansion).
+// Heavy causal blocks are launched first.  LSE is written in natural log.
+#include "fa_common.h"
+#include "kernels.h"
+
+namespace ema {
+namespace fa {
+namespace {
+
+constexpr int BM = 128;
+constexpr int BN = 64;
+constexpr int VPAD = 32;  // elements of padding per V row (64 B) -> conflict-free tr reads
+
+template <typename T, int HD, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_fwd_k(const AttnParams p) {
+  typedef typename MT<T>::x8 x8;
+  constexpr int KS = HD / 16;       // MFMA k-steps over head_dim
+  constexpr int DT = HD / 32;       // 32-wide d tiles of O
+  constexpr int CPR = HD / 8;       // 16-byte chunks per row
+  constexpr int VST = HD + VPAD;    // V row stride (elements)
+  constexpr int KCH = BN * CPR / 256;  // K (and V) chunks staged per thread
+  __shared__ __attribute__((aligned(16))) T k_lds[BN * HD];
+  __shared__ __attribute__((aligned(16))) T v_lds[BN * VST];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int nmb = (p.sq + BM - 1) / BM;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int r = p.nq / p.nkv, g = head / r;
+  const int off = p.sk - p.sq;  // bottom-right aligned causal mask
+
+  const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)(head % r) * p.q_sh;
+  const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
+  const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
+
+  const int m0 = mb * BM + wave * 32;
+  const int qrow = m0 + c;
+  const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;
+
+  x8 qf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
+
+  int n_end = p.sk;
+  if (CAUSAL) {
+    const int lim = mb * BM + BM + off;
+    n_end = lim < p.sk ? lim : p.sk;
+  }
+  const int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+
+  // staging registers: KCH chunks of K and of V for the next tile
+  x8 kst[KCH], vst[KCH];
+  auto load_tile = [&](int n0) {
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      int key = n0 + row;
+      key = key < p.sk ? key : p.sk - 1;
+      kst[i] = ld8(K + (int64_t)key * p.k_ss + ch * 8);
+      vst[i] = ld8(V + (int64_t)key * p.v_ss + ch * 8);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<x8*>(k_lds + sw_off<HD>(row, ch * 8)) = kst[i];
+      *reinterpret_cast<x8*>(v_lds + row * VST + ch * 8) = vst[i];
+    }
+  };
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+  const float sl2 = p.scale * 1.4426950408889634f;  // scale * log2(e)
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile();
+  }
+  __syncthreads();
+
+  // tr-read addressing (constant per lane)
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  for (int t = 0; t < ntiles; ++t) {
+    const int n0 = t * BN;
+    if (t + 1 < ntiles) load_tile(n0 + BN);
+
+    f32x16 s0, s1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s0[i] = s1[i] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const x8 ka0 = *reinterpret_cast<const x8*>(k_lds + sw_off<HD>(c, kk * 16 + 8 * h));
+      const x8 ka1 = *reinterpret_cast<const x8*>(k_lds + sw_off<HD>(32 + c, kk * 16 + 8 * h));
+      s0 = MT<T>::mfma(ka0, qf[kk], s0);
+      s1 = MT<T>::mfma(ka1, qf[kk], s1);
+    }
+    // scale (log2 domain) + mask
+    const bool need_mask = CAUSAL ? (n0 + BN - 1 > m0 + off) : (n0 + BN > p.sk);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s0[i] *= sl2;
+      s1[i] *= sl2;
+    }
+    if (need_mask) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k0 = n0 + acc_row(i, h), k1 = k0 + 32;
+        bool ok0 = k0 < p.sk, ok1 = k1 < p.sk;
+        if (CAUSAL) {
+          ok0 = ok0 && (k0 <= qrow + off);
+          ok1 = ok1 && (k1 <= qrow + off);
+        }
+        if (!ok0) s0[i] = -INFINITY;
+        if (!ok1) s1[i] = -INFINITY;
+      }
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_i, mt);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_i - m_use);
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s0[i] = exp2f(s0[i] - m_use);
+      s1[i] = exp2f(s1[i] - m_use);
+      rs += s0[i] + s1[i];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l_i = l_i * alpha + rs;
+    m_i = m_new;
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+
+    // O^T[d][q] += V^T[d][key] * P^T[key][q]
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const x8 pf = acc_frag<T>(sub == 0 ? s0 : s1, s);
+        const int krow = sub * 32 + 16 * s + 4 * h + tq;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const int col = d * 32 + (lane & 16) + 4 * tp;
+          const typename MT<T>::x4 va = MT<T>::tr_read(v_lds + krow * VST + col);
+          const typename MT<T>::x4 vb = MT<T>::tr_read(v_lds + (krow + 8) * VST + col);
+          o[d] = MT<T>::mfma(join<T>(va, vb), pf, o[d]);
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) store_tile();
+    __syncthreads();
+  }
+
+  // epilogue
+  if (qrow < p.sq) {
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    T* O = (T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow * p.o_ss + (int64_t)head * p.o_sh;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        typename MT<T>::x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (T)(o[d][4 * rg + e] * inv);
+        *reinterpret_cast<typename MT<T>::x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
+      }
+    }
+    if (h == 0) {
+      const float lse = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
+      p.lse[((int64_t)b * p.nq + head) * p.sq + qrow] = lse;
+    }
+  }
+}
+
+template <typename T, int HD>
+void launch_fwd(const AttnParams& p, hipStream_t s) {
+  dim3 grid((p.sq + BM - 1) / BM, p.nq, p.b);
+  if (p.causal)
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, true>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, false>), grid, dim3(256), 0, s, p);
+}
+
+}  // namespace
+}  // namespace fa
+
+bool flash_attn_supported(int hd, int dt) {
+  return (hd == 64 || hd == 128) && (dt == DT_BF16 || dt == DT_F16);
+}
+
+void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
+  if (dt == DT_BF16) {
+    if (p.hd == 128) fa::launch_fwd<bf16, 128>(p, s);
+    else fa::launch_fwd<bf16, 64>(p, s);
+  } else {
+    if (p.hd == 128) fa::launch_fwd<fp16, 128>(p, s);
+    else fa::launch_fwd<fp16, 64>(p, s);
+  }
+}
+
+}  // namespace ema

@@ -1,0 +1,99 @@
+// Host-side launcher declarations for the gfx950 kernels (implemented in *.hip).
+// Pointers are device pointers; `dt` is an ema::DType; no launcher synchronises.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ema {
+
+enum DType { DT_F32 = 0, DT_F16 = 1, DT_BF16 = 2 };
+
+// ---- norms.hip ---------------------------------------------------------------
+int norm_bwd_partials(int64_t rows);
+int norm_max_hidden(int dtype);
+void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
+                 float eps, int dt, hipStream_t s);
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                 float* dw_part, void* dw, int64_t rows, int H, int dt, hipStream_t s);
+void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
+                   float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s);
+void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
+                   const float* rstd, void* dx, float* dw_part, float* db_part, void* dw,
+                   void* db, int64_t rows, int H, int dt, hipStream_t s);
+
+// ---- rope.hip ----------------------------------------------------------------
+// In-place rotation of q (r heads per group) and k (1 head per group) of a
+// [s, b, ng, r+2, hd] tensor with element strides (ss, sb, sg, sh).
+void rope_qkv_inplace(void* qkv, const float* cos, const float* sin, const int64_t* pos,
+                      int64_t pos_stride_b, int S, int B, int G, int R, int HD, int64_t ss,
+                      int64_t sb, int64_t sg, int64_t sh, int offset, int inverse, int dt,
+                      hipStream_t s);
+
+// ---- activations.hip -----------------------------------------------------------
+void glu_fwd(const void* x, void* y, int64_t rows, int F, int kind, int dt, hipStream_t s);
+void glu_bwd(const void* dy, const void* x, void* dx, int64_t rows, int F, int kind, int dt,
+             hipStream_t s);
+void gelu_fwd(const void* x, const void* bias, void* y, int64_t rows, int F, int approx,
+              int dt, hipStream_t s);
+void gelu_bwd(const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int F,
+              int approx, int dt, hipStream_t s);
+
+// ---- cross_entropy.hip -----------------------------------------------------------
+void ce_fwd_fused(const void* logits, const int64_t* target, float* loss, float* lse,
+                  int64_t rows, int V, int dt, hipStream_t s);
+void ce_row_max(const void* logits, float* rmax, int64_t rows, int V, int dt, hipStream_t s);
+void ce_sumexp_target(const void* logits, const int64_t* target, const float* rmax,
+                      float* sumexp, float* tlogit, int64_t rows, int V, int64_t vstart, int dt,
+                      hipStream_t s);
+void ce_bwd(const void* logits, const int64_t* target, const float* lse, const float* dloss,
+            void* dlogits, int64_t rows, int V, int64_t vstart, int dt, hipStream_t s);
+
+// ---- softmax.hip -------------------------------------------------------------------
+// x [B, NP, SQ, SK]; mask (mode 2) uint8/bool [B, 1, SQ, SK]; mode 0 none, 1 causal.
+void softmax_fwd(const void* x, const uint8_t* mask, void* y, int64_t B, int64_t NP, int SQ,
+                 int SK, float scale, int mode, int dt, hipStream_t s);
+void softmax_bwd(const void* dy, const void* y, void* dx, int64_t rows, int SK, float scale,
+                 int dt, hipStream_t s);
+
+// ---- optim.hip ----------------------------------------------------------------------
+void chunked_sumsq(const float* grad, const int64_t* table, int n_chunks, float* partial,
+                   float* out, hipStream_t s);
+struct AdamArgs {
+  float lr[8];
+  float wd[8];
+  float beta1, beta2, eps, bc1, bc2, grad_scale;
+  int adam_w_mode;
+};
+void flat_adam(float* master, void* model_out, int model_dt, const float* grad, float* m,
+               float* v, const int64_t* table, int n_chunks, const AdamArgs& a, hipStream_t s);
+
+// ---- flash_attn_fwd.hip / flash_attn_bwd.hip -------------------------------------------------
+struct AttnParams {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;  // [b, nq, sq]
+  int b, sq, sk, nq, nkv, hd;
+  // element strides; query head j at (j / r) * q_sg + (j % r) * q_sh, kv group g at g * k_sg.
+  int64_t q_sb, q_ss, q_sg, q_sh;
+  int64_t k_sb, k_ss, k_sg;
+  int64_t v_sb, v_ss, v_sg;
+  int64_t o_sb, o_ss, o_sh;  // o / dout share strides
+  int causal;
+  float scale;
+};
+struct AttnBwdParams {
+  AttnParams f;
+  const void* dout;
+  void* dq;  // same strides as q
+  void* dk;  // same strides as k
+  void* dv;  // same strides as v
+  float* dq_acc;  // fp32 [b, nq, sq, hd] workspace (zeroed by the launcher)
+  float* delta;   // fp32 [b, nq, sq] workspace
+};
+void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
+void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
+bool flash_attn_supported(int hd, int dt);
+
+}  // namespace ema

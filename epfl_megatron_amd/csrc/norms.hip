@@ -1,0 +1,439 @@
+// RMSNorm / LayerNorm forward + backward for gfx950.
+//
+// Layout: x[rows, H] row-major.  One wave64 owns one row; the row is held in
+// registers as VPL 16-byte vectors per lane (VPL = ceil(H / (64 * 8)) for
+// bf16), so x is read from HBM exactly once in forward and once in backward.
+// 4 waves (256 threads) per workgroup -> rows/4 workgroups (>> 256 CUs for any
+// training shape).  Statistics in fp32.
+//
+// Weight/bias gradients: each wave accumulates its rows' contribution for all
+// H columns in registers, writes one fp32 partial row, and a second kernel
+// sums the partials column-wise in a fixed order (deterministic, no atomics).
+#include "common.h"
+#include "kernels.h"
+
+namespace ema {
+namespace {
+
+constexpr int kWaves = 4;
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
+                                                     const T* __restrict__ w, T* __restrict__ y,
+                                                     float* __restrict__ rstd_out, int64_t rows,
+                                                     int H, float eps) {
+  constexpr int N = V16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = H / N;
+  const T* xr = x + row * H;
+  V16<T> xv[VPL];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+      xv[i] = ld16(xr + vi * N);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float f = to_f(xv[i].v[e]);
+        ss += f * f;
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (lane == 0) rstd_out[row] = r;
+  T* yr = y + row * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+      const V16<T> wv = ld16(w + vi * N);
+      V16<T> o;
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        // reference numerics: normalise in fp32, round to T, then multiply by w.
+        const T xn = from_f<T>(to_f(xv[i].v[e]) * r);
+        o.v[e] = from_f<T>(to_f(xn) * to_f(wv.v[e]));
+      }
+      st16(yr + vi * N, o);
+    }
+  }
+}
+
+template <typename T, int VPL, bool DW>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy,
+                                                     const T* __restrict__ x,
+                                                     const T* __restrict__ w,
+                                                     const float* __restrict__ rstd,
+                                                     T* __restrict__ dx,
+                                                     float* __restrict__ dw_part, int64_t rows,
+                                                     int H) {
+  constexpr int N = V16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+  const int nvec = H / N;
+  float acc[VPL][N];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int e = 0; e < N; ++e) acc[i][e] = 0.f;
+  for (int64_t row = gw; row < rows; row += nwaves) {
+    const float r = rstd[row];
+    const T* xr = x + row * H;
+    const T* dyr = dy + row * H;
+    V16<T> xv[VPL], gv[VPL];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        xv[i] = ld16(xr + vi * N);
+        gv[i] = ld16(dyr + vi * N);
+        const V16<T> wv = ld16(w + vi * N);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const float xh = to_f(xv[i].v[e]) * r;
+          const float g = to_f(gv[i].v[e]);
+          dot += g * to_f(wv.v[e]) * xh;
+          if (DW) acc[i][e] += g * to_f(from_f<T>(xh));
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)H;
+    T* dxr = dx + row * H;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        const V16<T> wv = ld16(w + vi * N);
+        V16<T> o;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const float xh = to_f(xv[i].v[e]) * r;
+          o.v[e] = from_f<T>(r * (to_f(gv[i].v[e]) * to_f(wv.v[e]) - xh * dot));
+        }
+        st16(dxr + vi * N, o);
+      }
+    }
+  }
+  if (!DW) return;
+  float* part = dw_part + gw * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) part[vi * N + e] = acc[i][e];
+    }
+  }
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x,
+                                                       const T* __restrict__ w,
+                                                       const T* __restrict__ b,
+                                                       T* __restrict__ y, float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, int64_t rows,
+                                                       int H, float eps) {
+  constexpr int N = V16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = H / N;
+  const T* xr = x + row * H;
+  V16<T> xv[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+      xv[i] = ld16(xr + vi * N);
+#pragma unroll
+      for (int e = 0; e < N; ++e) s += to_f(xv[i].v[e]);
+    }
+  }
+  const float mu = wave_sum(s) / (float)H;
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float d = to_f(xv[i].v[e]) - mu;
+        var += d * d;
+      }
+    }
+  }
+  var = wave_sum(var) / (float)H;
+  const float r = rsqrtf(var + eps);
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = r;
+  }
+  T* yr = y + row * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+      const V16<T> wv = ld16(w + vi * N);
+      V16<T> bv;
+      if (b) bv = ld16(b + vi * N);
+      V16<T> o;
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        float v = (to_f(xv[i].v[e]) - mu) * r * to_f(wv.v[e]);
+        if (b) v += to_f(bv.v[e]);
+        o.v[e] = from_f<T>(v);
+      }
+      st16(yr + vi * N, o);
+    }
+  }
+}
+
+template <typename T, int VPL, bool DW>
+__global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy,
+                                                       const T* __restrict__ x,
+                                                       const T* __restrict__ w,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       T* __restrict__ dx,
+                                                       float* __restrict__ dw_part,
+                                                       float* __restrict__ db_part, int64_t rows,
+                                                       int H) {
+  constexpr int N = V16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+  const int nvec = H / N;
+  float aw[VPL][N], ab[VPL][N];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int e = 0; e < N; ++e) aw[i][e] = ab[i][e] = 0.f;
+  for (int64_t row = gw; row < rows; row += nwaves) {
+    const float mu = mean[row], r = rstd[row];
+    const T* xr = x + row * H;
+    const T* dyr = dy + row * H;
+    V16<T> xv[VPL], gv[VPL];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        xv[i] = ld16(xr + vi * N);
+        gv[i] = ld16(dyr + vi * N);
+        const V16<T> wv = ld16(w + vi * N);
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const float xh = (to_f(xv[i].v[e]) - mu) * r;
+          const float g = to_f(gv[i].v[e]);
+          const float gw_ = g * to_f(wv.v[e]);
+          sg += gw_;
+          sgx += gw_ * xh;
+          if (DW) {
+            aw[i][e] += g * xh;
+            ab[i][e] += g;
+          }
+        }
+      }
+    }
+    sg = wave_sum(sg) / (float)H;
+    sgx = wave_sum(sgx) / (float)H;
+    T* dxr = dx + row * H;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        const V16<T> wv = ld16(w + vi * N);
+        V16<T> o;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const float xh = (to_f(xv[i].v[e]) - mu) * r;
+          o.v[e] = from_f<T>(r * (to_f(gv[i].v[e]) * to_f(wv.v[e]) - sg - xh * sgx));
+        }
+        st16(dxr + vi * N, o);
+      }
+    }
+  }
+  if (!DW) return;
+  float* pw = dw_part + gw * H;
+  float* pb = db_part + gw * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        pw[vi * N + e] = aw[i][e];
+        pb[vi * N + e] = ab[i][e];
+      }
+    }
+  }
+}
+
+// Column-parallel weight-gradient partials for large H (the fused kernels keep
+// the dw accumulator in registers only while VPL <= 8): block (c, p) sums the
+// rows of chunk p for 2048 columns; partial rows are reduced by colsum_k.
+template <typename T, bool LN>
+__global__ __launch_bounds__(256) void norm_dw_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                 const float* __restrict__ mean,
+                                                 const float* __restrict__ rstd,
+                                                 float* __restrict__ dw_part,
+                                                 float* __restrict__ db_part, int64_t rows, int H,
+                                                 int64_t rows_per_chunk) {
+  constexpr int N = V16<T>::N;
+  const int col = (blockIdx.x * 256 + threadIdx.x) * N;
+  if (col >= H) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  float aw[N], ab[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) aw[e] = ab[e] = 0.f;
+  for (int64_t row = r0; row < r1; ++row) {
+    const float r = rstd[row];
+    const float mu = LN ? mean[row] : 0.f;
+    const V16<T> xv = ld16(x + row * H + col);
+    const V16<T> gv = ld16(dy + row * H + col);
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      const float g = to_f(gv.v[e]);
+      const float xh = (to_f(xv.v[e]) - mu) * r;
+      aw[e] += g * (LN ? xh : to_f(from_f<T>(xh)));
+      ab[e] += g;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    dw_part[(int64_t)blockIdx.y * H + col + e] = aw[e];
+    if (LN) db_part[(int64_t)blockIdx.y * H + col + e] = ab[e];
+  }
+}
+
+// Column sums of a [P, H] fp32 partial matrix -> out[H] (type T), fixed order.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_k(const float* __restrict__ part, T* __restrict__ out,
+                                                int P, int H) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= H) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(int64_t)p * H + j];
+  out[j] = from_f<T>(s);
+}
+
+template <typename T>
+int vec_elems() { return 16 / sizeof(T); }
+
+template <typename T>
+int pick_vpl(int H) {
+  const int per_lane = (H / vec_elems<T>() + 63) / 64;
+  if (per_lane <= 1) return 1;
+  if (per_lane <= 2) return 2;
+  if (per_lane <= 4) return 4;
+  if (per_lane <= 8) return 8;
+  if (per_lane <= 12) return 12;
+  if (per_lane <= 16) return 16;
+  return -1;
+}
+
+#define EMA_VPL_SWITCH(vpl, ...)                \
+  switch (vpl) {                                \
+    case 1: { constexpr int V = 1; __VA_ARGS__; break; }   \
+    case 2: { constexpr int V = 2; __VA_ARGS__; break; }   \
+    case 4: { constexpr int V = 4; __VA_ARGS__; break; }   \
+    case 8: { constexpr int V = 8; __VA_ARGS__; break; }   \
+    case 12: { constexpr int V = 12; __VA_ARGS__; break; } \
+    case 16: { constexpr int V = 16; __VA_ARGS__; break; } \
+  }
+
+}  // namespace
+
+int norm_bwd_partials(int64_t rows) {
+  int64_t blocks = (rows + kWaves - 1) / kWaves;
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks * kWaves;
+}
+
+int norm_max_hidden(int dtype) { return dtype == DT_F32 ? 16 * 64 * 4 : 16 * 64 * 8; }
+
+void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
+                 float eps, int dt, hipStream_t s) {
+  const int64_t blocks = (rows + kWaves - 1) / kWaves;
+  EMA_DISPATCH_FLOAT(dt, T, {
+    const int vpl = pick_vpl<T>(H);
+    EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_fwd_k<T, V>), dim3(blocks), dim3(256), 0, s,
+                                           (const T*)x, (const T*)w, (T*)y, rstd, rows, H, eps));
+  });
+}
+
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                 float* dw_part, void* dw, int64_t rows, int H, int dt, hipStream_t s) {
+  const int P = norm_bwd_partials(rows);
+  const int blocks = P / kWaves;
+  EMA_DISPATCH_FLOAT(dt, T, {
+    const int vpl = pick_vpl<T>(H);
+    if (vpl <= 8) {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, true>), dim3(blocks),
+                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
+                                             (const T*)w, rstd, (T*)dx, dw_part, rows, H));
+    } else {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, false>), dim3(blocks),
+                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
+                                             (const T*)w, rstd, (T*)dx, dw_part, rows, H));
+      const int64_t rpc = (rows + P - 1) / P;
+      const int cblocks = (H / (16 / (int)sizeof(T)) + 255) / 256;
+      hipLaunchKernelGGL((norm_dw_k<T, false>), dim3(cblocks, P), dim3(256), 0, s, (const T*)dy,
+                         (const T*)x, (const float*)nullptr, rstd, dw_part, (float*)nullptr,
+                         rows, H, rpc);
+    }
+    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, dw_part, (T*)dw,
+                       P, H);
+  });
+}
+
+void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
+                   float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s) {
+  const int64_t blocks = (rows + kWaves - 1) / kWaves;
+  EMA_DISPATCH_FLOAT(dt, T, {
+    const int vpl = pick_vpl<T>(H);
+    EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_fwd_k<T, V>), dim3(blocks), dim3(256), 0, s,
+                                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean,
+                                           rstd, rows, H, eps));
+  });
+}
+
+void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
+                   const float* rstd, void* dx, float* dw_part, float* db_part, void* dw,
+                   void* db, int64_t rows, int H, int dt, hipStream_t s) {
+  const int P = norm_bwd_partials(rows);
+  const int blocks = P / kWaves;
+  EMA_DISPATCH_FLOAT(dt, T, {
+    const int vpl = pick_vpl<T>(H);
+    if (vpl <= 8) {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_k<T, V, true>), dim3(blocks),
+                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
+                                             (const T*)w, mean, rstd, (T*)dx, dw_part, db_part,
+                                             rows, H));
+    } else {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_k<T, V, false>), dim3(blocks),
+                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
+                                             (const T*)w, mean, rstd, (T*)dx, dw_part, db_part,
+                                             rows, H));
+      const int64_t rpc = (rows + P - 1) / P;
+      const int cblocks = (H / (16 / (int)sizeof(T)) + 255) / 256;
+      hipLaunchKernelGGL((norm_dw_k<T, true>), dim3(cblocks, P), dim3(256), 0, s, (const T*)dy,
+                         (const T*)x, mean, rstd, dw_part, db_part, rows, H, rpc);
+    }
+    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, dw_part, (T*)dw,
+                       P, H);
+    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, db_part, (T*)db,
+                       P, H);
+  });
+}
+
+}  // namespace ema

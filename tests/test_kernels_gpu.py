@@ -1,0 +1,292 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference.
+
+Mirrors the intent of the reference's fused-kernel tests
+(megatron/fused_kernels/tests/test_fused_kernels.py) and extends them to the
+kernels the reference imported from external packages (flash-attn, apex).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ext():
+    from epfl_megatron_amd.ops._ext import ext
+    return ext()
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{msg}: {bad} elems off, max err {err.max().item():.3e}"
+
+
+def test_extension_loaded():
+    import epfl_megatron_amd._C as C
+    assert hasattr(C, "flash_attn_fwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("H", [256, 4096, 4544, 8192])
+def test_rmsnorm(dtype, H):
+    from epfl_megatron_amd.ops.norms import rms_norm, rms_norm_ref
+    torch.manual_seed(0)
+    x = torch.randn(37, 3, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(dtype).requires_grad_()
+    y = rms_norm(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = rms_norm_ref(xr, wr, 1e-5)
+    tol = 2e-2 if dtype != torch.float32 else 1e-5
+    _close(y, yr, tol, 1e-2, "rmsnorm fwd")
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    _close(x.grad, xr.grad, 5e-2 if dtype != torch.float32 else 1e-4, 2e-2, "rmsnorm dx")
+    _close(w.grad, wr.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "rmsnorm dw")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [768, 8192])
+def test_layernorm(dtype, H):
+    from epfl_megatron_amd.ops.norms import layer_norm
+    torch.manual_seed(1)
+    x = torch.randn(65, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(dtype).requires_grad_()
+    b = (0.1 * torch.randn(H, device=DEV)).to(dtype).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+    tol = 3e-2 if dtype != torch.float32 else 1e-4
+    _close(y, yr, tol, 1e-2, "layernorm fwd")
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    _close(x.grad, xr.grad, tol * 3, 2e-2, "layernorm dx")
+    _close(w.grad, wr.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "layernorm dw")
+    _close(b.grad, br.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "layernorm db")
+
+
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_rope_inplace(with_pos):
+    from epfl_megatron_amd.ops.rope import rope_table, rope_qkv_inplace, apply_rope_ref
+    torch.manual_seed(2)
+    s, b, g, r, hd = 33, 2, 4, 3, 128
+    qkv = torch.randn(s, b, g, r + 2, hd, device=DEV, dtype=torch.bfloat16)
+    cos, sin = rope_table(hd, 64, DEV)
+    pos = None
+    if with_pos:
+        pos = torch.randint(0, 64, (b, s), device=DEV)
+    ref = qkv.clone()
+    qk = ref[:, :, :, :r + 1].reshape(s, b, g * (r + 1), hd)
+    rot = apply_rope_ref(qk.float(), cos, sin, pos).view(s, b, g, r + 1, hd)
+    out = qkv.clone()
+    rope_qkv_inplace(out, cos, sin, pos)
+    _close(out[:, :, :, :r + 1], rot, 2e-2, 1e-2, "rope q/k")
+    assert torch.equal(out[:, :, :, r + 1], qkv[:, :, :, r + 1]), "v must be untouched"
+    back = out.clone()
+    rope_qkv_inplace(back, cos, sin, pos, inverse=True)
+    _close(back, qkv, 5e-2, 2e-2, "rope inverse")
+
+
+@pytest.mark.parametrize("kind", ["swiglu", "geglu", "reglu", "liglu"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_glu(kind, dtype):
+    from epfl_megatron_amd.ops.activations import glu, glu_ref
+    torch.manual_seed(3)
+    x = torch.randn(17, 5, 2 * 688, device=DEV, dtype=dtype, requires_grad=True)
+    y = glu(x, kind)
+    xr = x.detach().float().requires_grad_()
+    yr = glu_ref(xr, kind)
+    tol = 3e-2 if dtype != torch.float32 else 1e-5
+    _close(y, yr, tol, 1e-2, f"{kind} fwd")
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    _close(x.grad, xr.grad, tol * 2, 2e-2, f"{kind} bwd")
+
+
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_gelu(with_bias):
+    from epfl_megatron_amd.ops.activations import bias_gelu, bias_gelu_ref, gelu
+    torch.manual_seed(4)
+    x = torch.randn(64, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = (0.1 * torch.randn(1024, device=DEV)).bfloat16().requires_grad_() if with_bias else None
+    y = bias_gelu(b, x)
+    xr = x.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if with_bias else None
+    yr = bias_gelu_ref(br, xr)
+    _close(y, yr, 3e-2, 1e-2, "bias_gelu fwd")
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    _close(x.grad, xr.grad, 5e-2, 2e-2, "bias_gelu dx")
+    if with_bias:
+        _close(b.grad, br.grad, 0.5, 2e-2, "bias_gelu db")
+    x2 = x.detach().clone().requires_grad_()
+    y2 = gelu(x2)
+    _close(y2, torch.nn.functional.gelu(x2.float()), 3e-2, 1e-2, "erf gelu")
+
+
+@pytest.mark.parametrize("V", [512, 32000])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy(V, dtype):
+    from epfl_megatron_amd.ops.cross_entropy import vocab_parallel_cross_entropy
+    torch.manual_seed(5)
+    z = (3 * torch.randn(9, 4, V, device=DEV)).to(dtype).requires_grad_()
+    t = torch.randint(0, V, (9, 4), device=DEV)
+    loss = vocab_parallel_cross_entropy(z, t)
+    zr = z.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(zr.view(-1, V), t.view(-1), reduction="none").view(9, 4)
+    _close(loss, lr, 1e-3, 1e-4, "ce fwd")
+    g = torch.rand_like(loss)
+    loss.backward(g)
+    lr.backward(g)
+    _close(z.grad, zr.grad, 1e-2 if dtype != torch.float32 else 1e-6, 1e-2, "ce bwd")
+
+
+def test_cross_entropy_tp_pieces():
+    """Two-pass (TP>1) kernels combined on one device == full-vocab CE."""
+    torch.manual_seed(6)
+    e = _ext()
+    V, rows = 1024, 50
+    z = torch.randn(rows, V, device=DEV, dtype=torch.bfloat16)
+    t = torch.randint(0, V, (rows,), device=DEV)
+    halves = z.chunk(2, dim=1)
+    m = torch.stack([e.ce_row_max(h.contiguous()) for h in halves]).max(0)[0]
+    se, tl = 0, 0
+    for i, h in enumerate(halves):
+        a, b = e.ce_sumexp_target(h.contiguous(), t, m, i * (V // 2))
+        se, tl = se + a, tl + b
+    loss = torch.log(se) + m - tl
+    ref = torch.nn.functional.cross_entropy(z.float(), t, reduction="none")
+    _close(loss, ref, 1e-3, 1e-4, "ce tp")
+
+
+@pytest.mark.parametrize("mode", ["causal", "mask", "none"])
+@pytest.mark.parametrize("sk", [128, 1000, 4096])
+def test_fused_softmax(mode, sk):
+    from epfl_megatron_amd.ops.softmax import _SoftmaxFn
+    torch.manual_seed(7)
+    b, np_, sq = 2, 3, sk if mode == "causal" else 37
+    x = torch.randn(b, np_, sq, sk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    scale = 0.5
+    xf = x.detach().float() * scale
+    mask = None
+    if mode == "causal":
+        m = torch.ones(sq, sk, device=DEV, dtype=torch.bool).triu(1)
+        ref = torch.softmax(xf.masked_fill(m, float("-inf")), -1)
+        y = _SoftmaxFn.apply(x, None, scale, 1)
+    elif mode == "mask":
+        mask = torch.rand(b, 1, sq, sk, device=DEV) < 0.3
+        ref = torch.softmax(xf.masked_fill(mask, -10000.0), -1)
+        y = _SoftmaxFn.apply(x, mask, scale, 2)
+    else:
+        ref = torch.softmax(xf, -1)
+        y = _SoftmaxFn.apply(x, None, scale, 0)
+    _close(y, ref, 1e-2, 2e-2, f"softmax {mode}")
+    g = torch.randn_like(y)
+    y.backward(g)
+    yf = ref
+    dref = scale * yf * (g.float() - (g.float() * yf).sum(-1, keepdim=True))
+    _close(x.grad, dref, 2e-2, 3e-2, f"softmax bwd {mode}")
+
+
+def test_flat_adam_and_norm():
+    from epfl_megatron_amd.ops import optim_kernels as K
+    torch.manual_seed(8)
+    n = 300000
+    segs = [(0, 0, 100000, 0, True), (100032, 100032, 150000, 1, False),
+            (250048, 250048, 49952, 0, True)]
+    total = 300000
+    plan = K.ChunkPlan(segs, DEV)
+    grad = torch.randn(total, device=DEV)
+    master = torch.randn(total, device=DEV)
+    m = torch.randn(total, device=DEV).abs() * 0.1
+    v = torch.randn(total, device=DEV).abs() * 0.1
+    model = master.to(torch.bfloat16)
+    refs = [t.clone().cpu() for t in (master, m, v)]
+    nsq = K.grad_norm_sq(grad, plan)
+    cpu_plan = K.ChunkPlan(segs, "cpu")
+    nsq_ref = K.grad_norm_sq(grad.cpu(), cpu_plan)
+    assert abs(nsq.item() - nsq_ref.item()) / nsq_ref.item() < 1e-5
+    K.adam_step(master, model, grad, m, v, plan, [1e-3, 2e-3], [0.1, 0.0], 0.9, 0.95, 1e-8, 3, 0.7)
+    mr, m_r, v_r = refs
+    model_ref = torch.zeros(total, dtype=torch.bfloat16)
+    K.adam_step(mr, model_ref, grad.cpu(), m_r, v_r, cpu_plan, [1e-3, 2e-3], [0.1, 0.0], 0.9, 0.95,
+                1e-8, 3, 0.7)
+    _close(master.cpu(), mr, 1e-6, 1e-5, "adam master")
+    _close(m.cpu(), m_r, 1e-6, 1e-5, "adam m")
+    _close(v.cpu(), v_r, 1e-6, 1e-5, "adam v")
+    for lo, hi in ((0, 100000), (100032, 250032), (250048, 300000)):
+        _close(model[lo:hi].cpu(), mr[lo:hi].to(torch.bfloat16), 1e-2, 1e-2, "adam model write")
+
+
+def _attn_case(b, s, nq, nkv, hd, dtype, causal, seed=0):
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    torch.manual_seed(seed)
+    q = torch.randn(b, s, nq, hd, device=DEV, dtype=dtype, requires_grad=True)
+    k = torch.randn(b, s, nkv, hd, device=DEV, dtype=dtype, requires_grad=True)
+    v = torch.randn(b, s, nkv, hd, device=DEV, dtype=dtype, requires_grad=True)
+    o = flash_attn_func(q, k, v, causal=causal)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = attention_ref(qr, kr, vr, causal=causal)
+    _close(o, orf, 2e-2, 2e-2, "flash fwd")
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float())
+    _close(q.grad, qr.grad, 5e-2, 5e-2, "flash dq")
+    _close(k.grad, kr.grad, 5e-2, 5e-2, "flash dk")
+    _close(v.grad, vr.grad, 5e-2, 5e-2, "flash dv")
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("nq,nkv", [(4, 4), (8, 2), (4, 1)])
+def test_flash_attention(hd, causal, nq, nkv):
+    _attn_case(2, 256, nq, nkv, hd, torch.bfloat16, causal)
+
+
+@pytest.mark.parametrize("s", [1, 77, 200, 1000])
+def test_flash_attention_odd_lengths(s):
+    _attn_case(1, s, 4, 2, 128, torch.bfloat16, True, seed=s)
+
+
+def test_flash_attention_fp16():
+    _attn_case(1, 192, 4, 4, 128, torch.float16, True)
+
+
+def test_flash_attention_qkvpacked_rope():
+    """The training path: fused GQA QKV + in-place RoPE + FA, fwd and bwd."""
+    from epfl_megatron_amd.ops.attention import flash_attn_qkvpacked
+    from epfl_megatron_amd.ops.rope import rope_table
+    torch.manual_seed(9)
+    s, b, ng, r, hd = 300, 2, 2, 3, 128
+    cos, sin = rope_table(hd, 512, DEV)
+    x = torch.randn(s, b, ng * (r + 2) * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_qkvpacked(x.clone(), ng, r, hd, causal=True, rope=(cos, sin))
+    xr = x.detach().float().cpu().requires_grad_()
+    orf = flash_attn_qkvpacked(xr, ng, r, hd, causal=True, rope=(cos.cpu(), sin.cpu()))
+    _close(o.cpu(), orf, 3e-2, 3e-2, "qkvpacked fwd")
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float().cpu())
+    _close(x.grad.cpu(), xr.grad, 6e-2, 6e-2, "qkvpacked bwd")
+
+
+def test_flash_attention_kvcache_causal_offset():
+    """sq < sk (decode with cache): bottom-right aligned causal mask."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    torch.manual_seed(10)
+    q = torch.randn(2, 5, 8, 128, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(2, 70, 2, 128, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(2, 70, 2, 128, device=DEV, dtype=torch.bfloat16)
+    o = flash_attn_func(q, k, v, causal=True)
+    orf = attention_ref(q.float(), k.float(), v.float(), causal=True)
+    _close(o, orf, 2e-2, 2e-2, "kv-cache attention")
