@@ -337,6 +337,7 @@ int pick_vpl(int H) {
   if (per_lane <= 8) return 8;
   if (per_lane <= 12) return 12;
   if (per_lane <= 16) return 16;
+  if (per_lane <= 32) return 32;
   return -1;
 }
 
@@ -348,6 +349,7 @@ int pick_vpl(int H) {
     case 8: { constexpr int V = 8; __VA_ARGS__; break; }   \
     case 12: { constexpr int V = 12; __VA_ARGS__; break; } \
     case 16: { constexpr int V = 16; __VA_ARGS__; break; } \
+    case 32: { constexpr int V = 32; __VA_ARGS__; break; } \
   }
 
 }  // namespace
@@ -359,7 +361,7 @@ int norm_bwd_partials(int64_t rows) {
   return (int)blocks * kWaves;
 }
 
-int norm_max_hidden(int dtype) { return dtype == DT_F32 ? 16 * 64 * 4 : 16 * 64 * 8; }
+int norm_max_hidden(int dtype) { return dtype == DT_F32 ? 32 * 64 * 4 : 32 * 64 * 8; }
 
 void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
                  float eps, int dt, hipStream_t s) {
