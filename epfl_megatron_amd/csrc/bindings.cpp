@@ -69,7 +69,7 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   auto wc = as_dtype(w, x);
   auto dx = at::empty_like(x);
   auto dw = at::empty({H}, x.options());
-  const int P = ema::norm_bwd_partials(rows);
+  const int P = ema::norm_bwd_workspace_rows(rows);
   auto part = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     ema::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), rstd.data_ptr<float>(),
@@ -116,7 +116,7 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
   auto dx = at::empty_like(x);
   auto dw = at::empty({H}, x.options());
   auto db = at::empty({H}, x.options());
-  const int P = ema::norm_bwd_partials(rows);
+  const int P = ema::norm_bwd_workspace_rows(rows);
   auto pw = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   auto pb = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {

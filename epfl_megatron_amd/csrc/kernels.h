@@ -10,6 +10,7 @@ enum DType { DT_F32 = 0, DT_F16 = 1, DT_BF16 = 2 };
 
 // ---- norms.hip ---------------------------------------------------------------
 int norm_bwd_partials(int64_t rows);
+int norm_bwd_workspace_rows(int64_t rows);  // rows of the fp32 [*, H] partial workspace
 int norm_max_hidden(int dtype);
 void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
                  float eps, int dt, hipStream_t s);

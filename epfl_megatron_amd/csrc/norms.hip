@@ -315,14 +315,51 @@ __global__ __launch_bounds__(256) void norm_dw_k(const T* __restrict__ dy, const
 }
 
 // Column sums of a [P, H] fp32 partial matrix -> out[H] (type T), fixed order.
+// Stage 1: grid (H/64, kSplits), 256 threads = 64 columns x 4 row-lanes; each
+// block sums P/kSplits partial rows (coalesced 256-byte row segments) into
+// part2[split, H].  Stage 2: one thread per column adds the kSplits values.
+// (A one-thread-per-column loop over all P rows left ~4k threads on the whole
+// chip and took ~0.5 ms per call in the first MI355X profile.)
+constexpr int kSplits = 32;
+
+__global__ __launch_bounds__(256) void colsum_stage1_k(const float* __restrict__ part,
+                                                       float* __restrict__ part2, int P, int H) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int per = (P + kSplits - 1) / kSplits;
+  const int r0 = blockIdx.y * per;
+  const int r1 = r0 + per < P ? r0 + per : P;
+  float acc = 0.f;
+  if (col < H)
+    for (int r = r0 + rg; r < r1; r += 4) acc += part[(int64_t)r * H + col];
+  red[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && col < H) {
+    const int c = threadIdx.x & 63;
+    part2[(int64_t)blockIdx.y * H + col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_k(const float* __restrict__ part, T* __restrict__ out,
-                                                int P, int H) {
+__global__ __launch_bounds__(256) void colsum_stage2_k(const float* __restrict__ part2,
+                                                       T* __restrict__ out, int H) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= H) return;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(int64_t)p * H + j];
+#pragma unroll
+  for (int p = 0; p < kSplits; ++p) s += part2[(int64_t)p * H + j];
   out[j] = from_f<T>(s);
+}
+
+// part holds P + kSplits rows: [0, P) stage-1 input, [P, P + kSplits) stage-2 input.
+template <typename T>
+void colsum(float* part, T* out, int P, int H, hipStream_t s) {
+  float* part2 = part + (int64_t)P * H;
+  hipLaunchKernelGGL(colsum_stage1_k, dim3((H + 63) / 64, kSplits), dim3(256), 0, s, part,
+                     part2, P, H);
+  hipLaunchKernelGGL((colsum_stage2_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, part2, out,
+                     H);
 }
 
 template <typename T>
@@ -356,10 +393,12 @@ int pick_vpl(int H) {
 
 int norm_bwd_partials(int64_t rows) {
   int64_t blocks = (rows + kWaves - 1) / kWaves;
-  if (blocks > 512) blocks = 512;
+  if (blocks > 256) blocks = 256;
   if (blocks < 1) blocks = 1;
   return (int)blocks * kWaves;
 }
+
+int norm_bwd_workspace_rows(int64_t rows) { return norm_bwd_partials(rows) + kSplits; }
 
 int norm_max_hidden(int dtype) { return dtype == DT_F32 ? 32 * 64 * 4 : 32 * 64 * 8; }
 
@@ -393,8 +432,7 @@ void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd
                          (const T*)x, (const float*)nullptr, rstd, dw_part, (float*)nullptr,
                          rows, H, rpc);
     }
-    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, dw_part, (T*)dw,
-                       P, H);
+    colsum<T>(dw_part, (T*)dw, P, H, s);
   });
 }
 
@@ -431,10 +469,8 @@ void layernorm_bwd(const void* dy, const void* x, const void* w, const float* me
       hipLaunchKernelGGL((norm_dw_k<T, true>), dim3(cblocks, P), dim3(256), 0, s, (const T*)dy,
                          (const T*)x, mean, rstd, dw_part, db_part, rows, H, rpc);
     }
-    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, dw_part, (T*)dw,
-                       P, H);
-    hipLaunchKernelGGL((colsum_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, db_part, (T*)db,
-                       P, H);
+    colsum<T>(dw_part, (T*)dw, P, H, s);
+    colsum<T>(db_part, (T*)db, P, H, s);
   });
 }
 

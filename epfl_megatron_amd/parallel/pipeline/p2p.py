@@ -89,13 +89,20 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
     group = state.get_pipeline_model_parallel_group()
     prev_r = state.get_pipeline_model_parallel_prev_rank()
     next_r = state.get_pipeline_model_parallel_next_rank()
+    # Post order: activations (forward direction) before gradients (backward
+    # direction).  RCCL/NCCL match the point-to-point operations of one peer
+    # pair in posting order; with PP = 2 both messages of a combined
+    # send-forward/send-backward go to the SAME peer, so this order is what
+    # keeps "activation" matched with "activation" on the other side (the
+    # reference's order swapped them, which is why it forbade interleaving at
+    # PP = 2, megatron/arguments.py:117-120).
     ops = []
-    if tensor_send_prev is not None:
-        ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), prev_r, group))
-    if recv_prev_t is not None:
-        ops.append(dist.P2POp(dist.irecv, recv_prev_t, prev_r, group))
     if tensor_send_next is not None:
         ops.append(dist.P2POp(dist.isend, tensor_send_next.contiguous(), next_r, group))
+    if recv_prev_t is not None:
+        ops.append(dist.P2POp(dist.irecv, recv_prev_t, prev_r, group))
+    if tensor_send_prev is not None:
+        ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), prev_r, group))
     if recv_next_t is not None:
         ops.append(dist.P2POp(dist.irecv, recv_next_t, next_r, group))
     _p2p(ops)
