@@ -88,10 +88,74 @@ py::tuple blend_indices(py::array_t<double, py::array::c_style | py::array::forc
   return py::make_tuple(which, within);
 }
 
+// Sample assembly: for every requested sample id s, copy the token window
+// [sample_idx[s], sample_idx[s+1]] (inclusive end) out of the mapped corpus
+// into row r of an int64 [n, seq_length + 1] batch, walking doc_idx across
+// document boundaries.  Replaces the reference's per-sample Python loop of
+// np.concatenate (megatron/data/gpt_dataset.py:243-269); releases the GIL so
+// DataLoader worker threads scale.
+template <typename T>
+void stitch_impl(const T* tok, const int64_t* ptr, const int32_t* sz, const int32_t* di,
+                 int64_t n_di, const int32_t* si, int64_t n_si, const int64_t* samples,
+                 int64_t n, int64_t L, int64_t* out) {
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t s = samples[r];
+    if (s < 0 || s + 1 >= n_si) throw std::out_of_range("sample id out of range");
+    int64_t d = si[2 * s], off = si[2 * s + 1];
+    const int64_t d_end = si[2 * s + 2], off_end = si[2 * s + 3];
+    int64_t* o = out + r * L;
+    int64_t w = 0;
+    while (true) {
+      if (d >= n_di) throw std::out_of_range("doc_idx position out of range");
+      const int64_t item = di[d];
+      const T* src = tok + ptr[item] / (int64_t)sizeof(T);
+      const int64_t stop = (d == d_end) ? off_end + 1 : (int64_t)sz[item];
+      const int64_t cnt = stop - off;
+      if (cnt < 0 || w + cnt > L) throw std::length_error("sample window does not match seq_length");
+      for (int64_t i = 0; i < cnt; ++i) o[w + i] = (int64_t)src[off + i];
+      w += cnt;
+      if (d == d_end) break;
+      ++d;
+      off = 0;
+    }
+    if (w != L) throw std::length_error("sample shorter than seq_length + 1");
+  }
+}
+
+py::array_t<int64_t> stitch_samples(py::array tokens,
+                                    py::array_t<int64_t, py::array::c_style | py::array::forcecast> pointers,
+                                    py::array_t<int32_t, py::array::c_style | py::array::forcecast> sizes,
+                                    py::array_t<int32_t, py::array::c_style | py::array::forcecast> doc_idx,
+                                    py::array_t<int32_t, py::array::c_style | py::array::forcecast> sample_idx,
+                                    py::array_t<int64_t, py::array::c_style | py::array::forcecast> samples,
+                                    int64_t seq_length) {
+  const int64_t n = samples.size(), L = seq_length + 1;
+  py::array_t<int64_t> out({n, L});
+  int64_t* o = out.mutable_data();
+  const int64_t* p = pointers.data();
+  const int32_t* sz = sizes.data();
+  const int32_t* di = doc_idx.data();
+  const int32_t* si = sample_idx.data();
+  const int64_t* sm = samples.data();
+  const int64_t n_di = doc_idx.size(), n_si = sample_idx.size() / 2;
+  const char kind = tokens.dtype().kind();
+  const ssize_t isz = tokens.itemsize();
+  const void* t = tokens.data();
+  py::gil_scoped_release nogil;
+  if (kind == 'u' && isz == 2) stitch_impl((const uint16_t*)t, p, sz, di, n_di, si, n_si, sm, n, L, o);
+  else if (kind == 'u' && isz == 1) stitch_impl((const uint8_t*)t, p, sz, di, n_di, si, n_si, sm, n, L, o);
+  else if (kind == 'i' && isz == 4) stitch_impl((const int32_t*)t, p, sz, di, n_di, si, n_si, sm, n, L, o);
+  else if (kind == 'i' && isz == 8) stitch_impl((const int64_t*)t, p, sz, di, n_di, si, n_si, sm, n, L, o);
+  else if (kind == 'i' && isz == 2) stitch_impl((const int16_t*)t, p, sz, di, n_di, si, n_si, sm, n, L, o);
+  else throw std::invalid_argument("unsupported token dtype");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_helpers, m) {
   m.doc() = "dataset index builders";
   m.def("sample_index", &sample_index);
   m.def("blend_indices", &blend_indices);
+  m.def("stitch_samples", &stitch_samples);
 }

@@ -20,3 +20,13 @@ def build_blending_indices(dataset_index, dataset_sample_index, weights, num_dat
                                            int(size), bool(verbose))
     dataset_index[:] = which
     dataset_sample_index[:] = within
+
+
+def stitch_samples(tokens, pointers, sizes, doc_idx, sample_idx, samples, seq_length):
+    """int64 ``[len(samples), seq_length + 1]`` GPT samples gathered natively."""
+    return _helpers.stitch_samples(tokens, np.ascontiguousarray(pointers, dtype=np.int64),
+                                   np.ascontiguousarray(sizes, dtype=np.int32),
+                                   np.ascontiguousarray(doc_idx, dtype=np.int32),
+                                   np.ascontiguousarray(sample_idx, dtype=np.int32),
+                                   np.ascontiguousarray(np.atleast_1d(samples), dtype=np.int64),
+                                   int(seq_length))
