@@ -1,0 +1,178 @@
+"""Inference: KV-cached generation, scoring, beam search, sampling, REST API (CPU/gloo).
+
+The reference only tested serving manually.  Here the KV-cached incremental
+loop must reproduce a cache-free greedy decode (full re-forward each step),
+at TP=1, TP=2 and PP=2, and the REST contract is checked in-process.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+from dist_utils import run_dist, init_framework, TINY_LLAMA
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+PROMPTS = ["3 14 15 92 6", "5 35 8"]
+
+
+def _setup(argv):
+    import run_text_generation_server as srv
+    init_framework(argv, srv.add_text_generate_args)
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.training import get_model
+    from test_parallel_equivalence import _deterministic_init
+    from epfl_megatron_amd import get_args
+    model = get_model(srv.model_provider, ModelType.encoder_or_decoder, wrap_with_ddp=False)
+    _deterministic_init(model, get_args())
+    return model[0].eval()
+
+
+def _argv(extra=()):
+    a = [x for x in TINY_LLAMA if x not in ("--synthetic_data",)]
+    i = a.index("--model_name")
+    a = a[:i] + a[i + 2:]
+    return a + ["--model_name", "llama2", "--micro_batch_size", "1", "--global_batch_size", "1",
+                "--inference_batch_times_seqlen_threshold", "4"] + list(extra)
+
+
+def _generate(rank, world, extra, n):
+    model = _setup(_argv(extra))
+    from epfl_megatron_amd.inference import generate_and_post_process
+    out = generate_and_post_process(model, prompts=PROMPTS, tokens_to_generate=n,
+                                    return_output_log_probs=True, top_k_sampling=1,
+                                    use_eod_token_for_early_termination=False)
+    if out is None:
+        return None
+    texts, segs, logp, tokens = out
+    # cache-free reference decode on the same model (TP=PP=1 only)
+    return texts, logp, tokens
+
+
+def _reference_greedy(model, prompt_ids, n):
+    seq = list(prompt_ids)
+    logps = []
+    with torch.no_grad():
+        for _ in range(n):
+            t = torch.tensor([seq])
+            logits = model(t, None, None).float()
+            lp = torch.log_softmax(logits[0, -1], dim=-1)
+            nxt = int(torch.argmax(logits[0, -1]))
+            logps.append(float(lp[nxt]))
+            seq.append(nxt)
+    return seq, logps
+
+
+def _greedy_ref_run(rank, world, n):
+    model = _setup(_argv())
+    out = []
+    for p in PROMPTS:
+        ids = [int(x) for x in p.split()]
+        out.append(_reference_greedy(model, ids, n))
+    return out
+
+
+@pytest.fixture(scope="module")
+def greedy_ref():
+    return run_dist(_greedy_ref_run, 1, 6)[0]
+
+
+def _check_generation(res, ref, n=6):
+    texts, logp, tokens = res
+    for (want_seq, want_lp), got_tokens, got_lp, p in zip(ref, tokens, logp, PROMPTS):
+        plen = len(p.split())
+        assert got_tokens[plen:plen + n] == want_seq[plen:], (got_tokens, want_seq)
+        # generated-token log-probs follow the prompt-token ones
+        assert got_lp[plen - 1:plen - 1 + n] == pytest.approx(want_lp, abs=2e-4)
+
+
+def test_kv_cached_greedy_matches_full_forward(greedy_ref):
+    res = run_dist(_generate, 1, [], 6)[0]
+    _check_generation(res, greedy_ref)
+
+
+@pytest.mark.parametrize("extra,world", [(["--tensor_model_parallel_size", "2"], 2),
+                                         (["--pipeline_model_parallel_size", "2"], 2)])
+def test_parallel_generation_matches(greedy_ref, extra, world):
+    res = [r for r in run_dist(_generate, world, extra, 6) if r is not None][0]
+    _check_generation(res, greedy_ref)
+
+
+def _score_and_beam(rank, world):
+    model = _setup(_argv())
+    from epfl_megatron_amd.inference import generate, beam_search_and_post_process
+    toks, lens, logp = generate(model, prompts=["3 14 15 92 6"], tokens_to_generate=0)
+    with torch.no_grad():
+        full = torch.log_softmax(model(toks, None, None).float(), dim=-1)
+    want = torch.gather(full[:, :-1], 2, toks[:, 1:].unsqueeze(2)).squeeze(2)
+    texts, segs, scores = beam_search_and_post_process(model, prompts=["3 14 15"],
+                                                       tokens_to_generate=5, beam_size=3,
+                                                       stop_token=249, num_return_gen=3)
+    return logp, want, texts, scores
+
+
+def test_scoring_and_beam_search():
+    logp, want, texts, scores = run_dist(_score_and_beam, 1)[0]
+    torch.testing.assert_close(logp, want, atol=1e-5, rtol=1e-5)
+    assert len(texts) == 3 and all(t.startswith("3 14 15") for t in texts)
+    assert scores == sorted(scores, reverse=True)
+
+
+def test_sampling_filters():
+    from epfl_megatron_amd.inference.sampling import sample
+    torch.manual_seed(0)
+    logits = torch.tensor([[0.0, 1.0, 2.0, 3.0, 4.0]] * 256)
+    assert sample(logits, top_k=1).unique().tolist() == [4]
+    s = sample(logits, top_k=2)
+    assert set(s.unique().tolist()) <= {3, 4}
+    # top_p=0.5: sorted probs [.636, .234, ...]; keep the first token that crosses p
+    s = sample(logits, top_p=0.5)
+    assert s.unique().tolist() == [4]
+    s = sample(logits, top_p=0.8)
+    assert set(s.unique().tolist()) <= {3, 4}
+    assert sample(logits, top_k=1, vocab_size=3).unique().tolist() == [2]
+
+
+def test_request_validation():
+    from epfl_megatron_amd.inference.server import RequestError, parse_request
+    kind, kw, _ = parse_request({"prompts": ["a"], "tokens_to_generate": 4, "top_p": 0.9})
+    assert kind == "generate" and kw["top_p_sampling"] == 0.9
+    kind, kw, _ = parse_request({"prompts": ["a"], "beam_width": 2})
+    assert kind == "beam" and kw["beam_size"] == 2
+    for bad, msg in [({}, "prompts argument required"),
+                     ({"prompts": []}, "prompts is empty"),
+                     ({"prompts": ["a"] * 129}, "Maximum number of prompts is 128"),
+                     ({"prompts": ["a"], "max_len": 3}, "max_len is no longer used"),
+                     ({"prompts": ["a"], "tokens_to_generate": 0}, "implies logprobs"),
+                     ({"prompts": ["a"], "top_k": 5, "top_p": 0.5}, "cannot set both"),
+                     ({"prompts": ["a"], "top_p_decay": 0.5}, "cannot be set without top_p"),
+                     ({"prompts": [""]}, "Empty prompts require add_BOS"),
+                     ({"prompts": ["a", "b"], "beam_width": 2}, "batch size must be 1"),
+                     ({"prompts": ["a"], "temperature": 0}, "temperature must be")]:
+        with pytest.raises(RequestError, match=msg):
+            parse_request(bad)
+
+
+def _rest(rank, world):
+    model = _setup(_argv())
+    from fastapi.testclient import TestClient
+    from epfl_megatron_amd.inference.server import MegatronServer
+    client = TestClient(MegatronServer(model).app)
+    ok = client.put("/api", json={"prompts": ["3 14 15"], "tokens_to_generate": 3, "top_k": 1,
+                                  "logprobs": True, "no_log": True})
+    bad = client.put("/api", json={"prompts": "x"})
+    beam = client.put("/api", json={"prompts": ["3 14"], "tokens_to_generate": 2,
+                                    "beam_width": 2, "stop_token": 249, "no_log": True})
+    return ok.status_code, ok.json(), bad.status_code, bad.text, beam.status_code, beam.json()
+
+
+def test_rest_api():
+    pytest.importorskip("fastapi")
+    pytest.importorskip("httpx")
+    ok_code, ok, bad_code, bad, beam_code, beam = run_dist(_rest, 1)[0]
+    assert ok_code == 200 and ok["text"][0].startswith("3 14 15")
+    assert len(ok["segments"][0]) == len(ok["logprobs"][0]) + 1
+    assert bad_code == 400 and "not a list" in bad
+    assert beam_code == 200 and len(beam["scores"]) == 2
