@@ -60,10 +60,12 @@ def build_kernels(force=False, jobs=None):
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
             jobs_list.append([HIPCC, "-c", src, "-o", obj] + common)
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.cpp.o")
-    objs.append(bobj)
-    if force or _newer(bobj, [bsrc] + headers):
+    # host-side sources that use ATen / pybind11 / hipBLASLt
+    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "gemm_lt.cpp")):
+        bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if not (force or _newer(bobj, [bsrc] + headers)):
+            continue
         cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-O2", "-std=c++17", "-fPIC", "-I", CSRC,
                f"--offload-arch={ARCH}",
                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
@@ -80,7 +82,8 @@ def build_kernels(force=False, jobs=None):
     if force or jobs_list or not os.path.exists(out):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs +
              ["-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-              "-ltorch_python", f"-Wl,-rpath,{lib}"])
+              "-ltorch_python", f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib", "-lhipblaslt",
+             "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 

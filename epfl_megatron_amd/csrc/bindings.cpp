@@ -452,9 +452,43 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 
+// ---------------------------------------------------------------- wgrad GEMM
+bool wgrad_supported(int64_t M, int64_t N, int64_t K) { return ema::wgrad_supported(M, N, K); }
+
+// main_grad[N,K] (+)= dy[M,N]^T x[M,K]
+void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool accumulate) {
+  check_gpu(dy, "dy");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && g.dim() == 2, "wgrad_gemm: 2-D operands");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && g.is_contiguous(),
+              "wgrad_gemm: contiguous operands required");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && g.scalar_type() == at::kFloat,
+              "wgrad_gemm: dy/x same 16-bit dtype, g fp32");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && g.size(0) == N && g.size(1) == K, "wgrad_gemm: shape mismatch");
+  TORCH_CHECK(ema::wgrad_supported(M, N, K), "wgrad_gemm: unsupported shape");
+  const int dt = dtype_code(dy);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "wgrad_gemm: bf16/fp16 only");
+  ema::wgrad_gemm(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), M, N, K, accumulate, dt,
+                  cur_stream());
+}
+
+void wgrad_gemm_ablation(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, int64_t mode) {
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "ablation builds are bf16 only");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(ema::wgrad_supported(M, N, K) && g.numel() == N * K, "unsupported shape");
+  ema::wgrad_gemm_ablation(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), M, N, K, (int)mode,
+                           cur_stream());
+}
+
 }  // namespace
 
+void register_gemm_lt(pybind11::module& m);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_gemm_lt(m);
+  m.def("wgrad_gemm", &wgrad_gemm);
+  m.def("wgrad_supported", &wgrad_supported);
+  m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

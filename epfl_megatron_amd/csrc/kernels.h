@@ -95,6 +95,14 @@ struct AttnBwdParams {
 };
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
+
+// ---- gemm_wgrad.hip ------------------------------------------------------------------------------
+// G[N,K] (+)= dY[M,N]^T X[M,K]; dY/X bf16|fp16 row-major, G fp32 row-major.
+bool wgrad_supported(int64_t M, int64_t N, int64_t K);
+void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
+                bool accumulate, int dt, hipStream_t s);
+void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
+                         int64_t K, int mode, hipStream_t s);
 bool flash_attn_supported(int hd, int dt);
 
 }  // namespace ema

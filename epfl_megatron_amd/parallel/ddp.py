@@ -137,10 +137,22 @@ class DistributedDataParallel(torch.nn.Module):
     def _make_accum_hook(self, p):
         def hook(param):
             if param.grad is not None:
-                param.main_grad.add_(param.grad.view_as(param.main_grad))
+                g = param.grad.view_as(param.main_grad)
+                if getattr(param, "_mg_fresh", False):
+                    param.main_grad.copy_(g)
+                    param._mg_fresh = False
+                else:
+                    param.main_grad.add_(g)
                 param.grad = None
             self._mark_ready(param)
         return hook
+
+    def _zero_untouched(self, params=None):
+        """main_grad of params that got no gradient this step (still fresh) -> 0."""
+        for p in (self.param_index if params is None else params):
+            if getattr(p, "_mg_fresh", False):
+                p.main_grad.zero_()
+                p._mg_fresh = False
 
     def _make_ready_cb(self, p):
         def cb():
@@ -164,19 +176,24 @@ class DistributedDataParallel(torch.nn.Module):
 
     def _launch(self, b):
         data = self._bucket_view(b)
+        # RCCL averages in the reduction itself (ncclAvg): no separate 1/dp pass
+        # over the bucket.  gloo has no AVG: pre-divide there.
+        if self._is_gloo:
+            data.div_(self.dp_size)
+            op = dist.ReduceOp.SUM
+        else:
+            op = dist.ReduceOp.AVG
         if self.use_distributed_optimizer:
             out = data[self.dp_rank * b.shard_size:(self.dp_rank + 1) * b.shard_size]
             if self._is_gloo:
-                data.div_(self.dp_size)
                 comm.reduce_scatter_into(out, data, group=self.dp_group)
                 b.handle = None
             else:
-                data.div_(self.dp_size)
-                b.handle = dist.reduce_scatter_tensor(out, data, group=self.dp_group,
+                b.handle = dist.reduce_scatter_tensor(out, data, op=op, group=self.dp_group,
                                                       async_op=True)
         else:
-            data.div_(self.dp_size)
-            b.handle = dist.all_reduce(data, group=self.dp_group, async_op=not self._is_gloo)
+            b.handle = dist.all_reduce(data, op=op, group=self.dp_group,
+                                       async_op=not self._is_gloo)
             if self._is_gloo:
                 b.handle = None
         b.pending = -1  # launched
@@ -184,10 +201,12 @@ class DistributedDataParallel(torch.nn.Module):
     def finish_grad_sync(self):
         """Launch any bucket not yet launched, then wait for all of them."""
         if self.dp_size == 1:
+            self._zero_untouched()
             self._reset_pending()
             return
         for b in self.buckets:
             if b.pending != -1:
+                self._zero_untouched(b.params)
                 self._launch(b)
         for b in self.buckets:
             if b.handle is not None:
@@ -211,7 +230,12 @@ class DistributedDataParallel(torch.nn.Module):
         self._sync_enabled = enabled
 
     def zero_grad_buffer(self):
-        self.grad_buffer.zero_()
+        """Lazy zeroing: mark every main_grad "fresh".  The first contribution of
+        the step then overwrites instead of accumulating (the wgrad GEMM stores
+        with beta = 0, hooks copy), and params that receive no gradient are
+        zeroed before their bucket is reduced — no 4-bytes/param fill pass."""
+        for p in self.param_index:
+            p._mg_fresh = True
         self._reset_pending()
 
     def broadcast_params(self):

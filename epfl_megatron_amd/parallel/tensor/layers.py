@@ -7,12 +7,13 @@ not split.
 
 MI355X-specific design of the GEMM path (``_LinearFn``):
 
-* GEMMs run on hipBLASLt through ``torch.matmul``.
-* With ``gradient_accumulation_fusion`` the weight gradient is produced by a
-  bf16 x bf16 -> fp32 GEMM written **in place** into the fp32 ``main_grad``
-  view of the DDP bucket (beta = 1, ``torch.addmm(..., out_dtype=float32,
-  out=main_grad)``) — no separate wgrad tensor and no accumulate kernel
-  (reference N8 / apex ``fused_weight_gradient_mlp_cuda``).  Immediately after
+* Forward and dgrad GEMMs run on hipBLASLt through ``torch.matmul``.
+* With ``gradient_accumulation_fusion`` the weight gradient is produced by the
+  hand-written gfx950 MFMA kernel ``csrc/gemm_wgrad.hip`` (bf16 x bf16 -> fp32)
+  written **in place** into the fp32 ``main_grad`` view of the DDP bucket —
+  no separate wgrad tensor, no accumulate kernel, and no zero-fill (the first
+  micro-batch stores with beta = 0; reference N8 / apex
+  ``fused_weight_gradient_mlp_cuda``).  Immediately after
   enqueueing it we signal the DDP bucket manager, which can start that
   bucket's RCCL reduction while backward continues (the reference only
   reduces after the whole backward).
@@ -22,6 +23,7 @@ MI355X-specific design of the GEMM path (``_LinearFn``):
   ordering comes from events, not from ``CUDA_DEVICE_MAX_CONNECTIONS``).
 """
 import math
+import os
 import warnings
 
 import torch
@@ -37,6 +39,7 @@ from .mappings import (copy_to_tensor_model_parallel_region,
                        scatter_to_tensor_model_parallel_region)
 from .random import get_cuda_rng_tracker
 from .utils import VocabUtility
+from ...ops._ext import ext
 
 _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {
     "tensor_model_parallel": False,
@@ -152,13 +155,39 @@ def _notify_grad_ready(param):
         cb()
 
 
-def _wgrad_into_main_grad(main_grad, grad_output_2d, input_2d):
-    """main_grad[out, in] += dY^T @ X with fp32 accumulation, in place."""
+# Weight-gradient GEMM backend.  EMA_WGRAD=hip selects the hand-written MFMA
+# kernel; the default stays hipBLASLt while it measures faster in the full
+# 7B step (profiles/r1_wgrad_ab.txt: 22.90k vs 22.24k tokens/s on 1 MI355X,
+# the kernel reaching ~1000 TFLOP/s like hipBLASLt in isolation).
+_WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hipblaslt").lower() == "hip"
+
+
+def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
+    """main_grad[out, in] (+)= dY^T @ X with fp32 accumulation, in place.
+
+    ``weight._mg_fresh`` (set by ``DistributedDataParallel.zero_grad_buffer``
+    instead of zero-filling the buffer) makes the first contribution of a step
+    a plain store (beta = 0): no fill kernel, no read of the old values.  On
+    the GPU the hand-written MFMA kernel (``csrc/gemm_wgrad.hip``) is used for
+    every shape it tiles; others go to hipBLASLt through ``torch.addmm``.
+    """
+    main_grad = weight.main_grad
+    accumulate = not getattr(weight, "_mg_fresh", False)
+    weight._mg_fresh = False
     if main_grad.is_cuda and grad_output_2d.dtype in (torch.bfloat16, torch.float16):
-        torch.addmm(main_grad, grad_output_2d.t(), input_2d, out_dtype=torch.float32,
-                    out=main_grad)
-    else:
+        M, N = grad_output_2d.shape
+        K = input_2d.shape[1]
+        if _WGRAD_KERNEL and main_grad.is_contiguous() and grad_output_2d.is_contiguous() \
+                and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K):
+            ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
+        else:
+            torch.addmm(main_grad, grad_output_2d.t(), input_2d, beta=1.0 if accumulate else 0.0,
+                        out_dtype=torch.float32, out=main_grad)
+    elif accumulate:
         main_grad.addmm_(grad_output_2d.t().to(main_grad.dtype), input_2d.to(main_grad.dtype))
+    else:
+        torch.mm(grad_output_2d.t().to(main_grad.dtype), input_2d.to(main_grad.dtype),
+                 out=main_grad)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -213,7 +242,7 @@ class _LinearFn(torch.autograd.Function):
             handle = comm.reduce_scatter_into(sub_grad_input, grad_input, group=tp_group,
                                               async_op=True)
         if ctx.gradient_accumulation_fusion and hasattr(weight, "main_grad"):
-            _wgrad_into_main_grad(weight.main_grad, go2, ti2)
+            _wgrad_into_main_grad(weight, go2, ti2)
             grad_weight = None
             _notify_grad_ready(weight)
         else:

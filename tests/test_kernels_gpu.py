@@ -290,3 +290,58 @@ def test_flash_attention_kvcache_causal_offset():
     o = flash_attn_func(q, k, v, causal=True)
     orf = attention_ref(q.float(), k.float(), v.float(), causal=True)
     _close(o, orf, 2e-2, 2e-2, "kv-cache attention")
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 256, 256), (96, 512, 256), (1024, 768, 512),
+                                   (8192, 256, 512)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_wgrad_gemm(M, N, K, dtype):
+    """Hand-written MFMA wgrad (csrc/gemm_wgrad.hip) vs fp32 reference, beta 1 and 0."""
+    C = _ext()
+    torch.manual_seed(0)
+    dy = torch.randn(M, N, device=DEV, dtype=dtype)
+    x = torch.randn(M, K, device=DEV, dtype=dtype)
+    g = torch.randn(N, K, device=DEV, dtype=torch.float32)
+    ref = g + dy.float().t() @ x.float()
+    assert C.wgrad_supported(M, N, K)
+    C.wgrad_gemm(dy, x, g, True)
+    _close(g, ref, atol=1e-3 * math.sqrt(M), msg="accumulate")
+    g2 = torch.full((N, K), float("nan"), device=DEV)
+    C.wgrad_gemm(dy, x, g2, False)
+    _close(g2, dy.float().t() @ x.float(), atol=1e-3 * math.sqrt(M), msg="store")
+    assert not C.wgrad_supported(M, N + 128, K)
+
+
+def test_lt_gemm_layouts():
+    """hipBLASLt wrapper with explicit solution selection: all three training layouts."""
+    C = _ext()
+    torch.manual_seed(1)
+    M, N, K = 256, 384, 512
+    X = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    W = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    dY = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    algos = C.lt_algos(X, False, W, True, Y, 0.0, 4)
+    assert algos
+    C.lt_gemm(X, False, W, True, Y, 1.0, 0.0, algos[-1])
+    _close(Y, X.float() @ W.float().t(), atol=0.5, rtol=2e-2, msg="fwd")
+    G = torch.randn(N, K, device=DEV)
+    G0 = G.clone()
+    C.lt_gemm(dY, True, X, False, G, 1.0, 1.0, -1)
+    _close(G, G0 + dY.float().t() @ X.float(), atol=0.05, rtol=1e-3, msg="wgrad")
+
+
+def test_linear_wgrad_fresh_and_accumulate():
+    """_LinearFn wgrad path: fresh main_grad stores, later micro-batches accumulate."""
+    from epfl_megatron_amd.parallel.tensor.layers import _wgrad_into_main_grad
+    torch.manual_seed(2)
+    w = torch.nn.Parameter(torch.randn(512, 256, device=DEV, dtype=torch.bfloat16))
+    w.main_grad = torch.full((512, 256), 7.0, device=DEV)
+    w._mg_fresh = True
+    ref = torch.zeros(512, 256, device=DEV)
+    for _ in range(3):
+        dy = torch.randn(128, 512, device=DEV, dtype=torch.bfloat16)
+        x = torch.randn(128, 256, device=DEV, dtype=torch.bfloat16)
+        _wgrad_into_main_grad(w, dy, x)
+        ref += dy.float().t() @ x.float()
+    _close(w.main_grad, ref, atol=0.05, msg="main_grad")
