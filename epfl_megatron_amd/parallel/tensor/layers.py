@@ -7,7 +7,9 @@ not split.
 
 MI355X-specific design of the GEMM path (``_LinearFn``):
 
-* Forward and dgrad GEMMs run on hipBLASLt through ``torch.matmul``.
+* Forward, dgrad and wgrad GEMMs run on hipBLASLt through PyTorch
+  (``EMA_GEMM=tuned`` switches to ``ops/gemm.py``'s per-shape solution
+  timing; ``EMA_WGRAD=hip`` to the hand-written MFMA wgrad kernel).
 * With ``gradient_accumulation_fusion`` the weight gradient is produced by the
   hand-written gfx950 MFMA kernel ``csrc/gemm_wgrad.hip`` (bf16 x bf16 -> fp32)
   written **in place** into the fp32 ``main_grad`` view of the DDP bucket —
@@ -40,6 +42,7 @@ from .mappings import (copy_to_tensor_model_parallel_region,
 from .random import get_cuda_rng_tracker
 from .utils import VocabUtility
 from ...ops._ext import ext
+from ...ops import gemm as tuned_gemm
 
 _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {
     "tensor_model_parallel": False,
@@ -160,6 +163,11 @@ def _notify_grad_ready(param):
 # 7B step (profiles/r1_wgrad_ab.txt: 22.90k vs 22.24k tokens/s on 1 MI355X,
 # the kernel reaching ~1000 TFLOP/s like hipBLASLt in isolation).
 _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hipblaslt").lower() == "hip"
+# EMA_GEMM=tuned routes all three products through ops/gemm.py (per-shape
+# solution timing).  Off by default: in the full 7B step it measured 22.4k vs
+# 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —
+# isolated timings with hot caches do not predict in-model kernel times.
+_TUNED_GEMM = os.environ.get("EMA_GEMM", "torch").lower() == "tuned"
 
 
 def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
@@ -180,6 +188,8 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
         if _WGRAD_KERNEL and main_grad.is_contiguous() and grad_output_2d.is_contiguous() \
                 and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K):
             ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
+        elif _TUNED_GEMM:
+            tuned_gemm.wgrad(main_grad.view(N, K), grad_output_2d, input_2d, accumulate)
         else:
             torch.addmm(main_grad, grad_output_2d.t(), input_2d, beta=1.0 if accumulate else 0.0,
                         out_dtype=torch.float32, out=main_grad)
@@ -206,7 +216,11 @@ class _LinearFn(torch.autograd.Function):
             comm.all_gather_into(total, input_, group=state.get_tensor_model_parallel_group())
         else:
             total = input_
-        out = torch.matmul(total, weight.t())
+        if total.is_cuda and _TUNED_GEMM:
+            x2 = total.reshape(-1, total.shape[-1])
+            out = tuned_gemm.linear_fwd(x2, weight).view(*total.shape[:-1], weight.shape[0])
+        else:
+            out = torch.matmul(total, weight.t())
         if bias is not None:
             out = out + bias
         return out
@@ -224,7 +238,12 @@ class _LinearFn(torch.autograd.Function):
             gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
         else:
             total = input_
-        grad_input = grad_output.matmul(weight)
+        if grad_output.is_cuda and _TUNED_GEMM:
+            g2 = grad_output.reshape(-1, grad_output.shape[-1])
+            grad_input = tuned_gemm.linear_dgrad(g2, weight).view(
+                *grad_output.shape[:-1], weight.shape[1])
+        else:
+            grad_input = grad_output.matmul(weight)
         if gather_handle is not None:
             gather_handle.wait()
         go2 = grad_output.reshape(-1, grad_output.shape[-1])

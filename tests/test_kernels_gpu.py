@@ -345,3 +345,21 @@ def test_linear_wgrad_fresh_and_accumulate():
         _wgrad_into_main_grad(w, dy, x)
         ref += dy.float().t() @ x.float()
     _close(w.main_grad, ref, atol=0.05, msg="main_grad")
+
+
+def test_tuned_gemm_products(tmp_path, monkeypatch):
+    """ops/gemm.py: tuned forward/dgrad/wgrad agree with fp32 references."""
+    monkeypatch.setenv("EMA_GEMM_CACHE", str(tmp_path))
+    from epfl_megatron_amd.ops import gemm
+    torch.manual_seed(3)
+    x = torch.randn(512, 256, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(384, 256, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(512, 384, device=DEV, dtype=torch.bfloat16)
+    _close(gemm.linear_fwd(x, w), x.float() @ w.float().t(), atol=0.5, rtol=2e-2, msg="fwd")
+    _close(gemm.linear_dgrad(dy, w), dy.float() @ w.float(), atol=0.5, rtol=2e-2, msg="dgrad")
+    g = torch.full((384, 256), float("nan"), device=DEV)
+    gemm.wgrad(g, dy, x, False)
+    ref = dy.float().t() @ x.float()
+    _close(g, ref, atol=0.05, rtol=1e-3, msg="wgrad store")
+    gemm.wgrad(g, dy, x, True)
+    _close(g, 2 * ref, atol=0.1, rtol=1e-3, msg="wgrad accumulate")
