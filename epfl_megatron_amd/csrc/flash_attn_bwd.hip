@@ -110,36 +110,58 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_k(const AttnBwdParams P) {
   }
   constexpr int QCH = 2 * BQ * CPR / 256;  // Q + dO chunks staged per thread
 
-  for (int hh = 0; hh < r; ++hh) {
+  // Flat (head, query-tile) step loop.  The next step's Q / dO / LSE / delta
+  // are register-staged (issued right after this step's LDS image is written)
+  // so their HBM latency hides behind this step's 40 MFMAs instead of
+  // stalling the single wave per SIMD every step (CDNA guide T14).
+  const int nsteps_q = p.sq > q_first ? (p.sq - q_first + BQ - 1) / BQ : 0;
+  const int nsteps = r * nsteps_q;
+  x8 qst[QCH];
+  float lse_st = 0.f, dl_st = 0.f;
+  auto prefetch = [&](int step) {
+    const int hh = step / nsteps_q;
+    const int q0 = q_first + (step - hh * nsteps_q) * BQ;
     const int head = g * r + hh;
     const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)hh * p.q_sh;
     const T* DO = (const T*)P.dout + (int64_t)b * p.o_sb + (int64_t)head * p.o_sh;
-    const float* LSE = p.lse + ((int64_t)b * p.nq + head) * p.sq;
-    const float* DL = P.delta + ((int64_t)b * p.nq + head) * p.sq;
-    float* DQ = P.dq_acc + ((int64_t)b * p.nq + head) * (int64_t)p.sq * HD;
+#pragma unroll
+    for (int i = 0; i < QCH; ++i) {
+      const bool is_do = i >= QCH / 2;  // chunks [0, QCH/2): Q, then dO
+      const int rem = tid + 256 * (i - (is_do ? QCH / 2 : 0));
+      const int row = rem / CPR, ch = rem % CPR;
+      int qr = q0 + row;
+      qr = qr < p.sq ? qr : p.sq - 1;
+      qst[i] = is_do ? ld8(DO + (int64_t)qr * p.o_ss + ch * 8)
+                     : ld8(Q + (int64_t)qr * p.q_ss + ch * 8);
+    }
+    if (tid < BQ) {
+      const int qr = q0 + tid;
+      const int64_t rb = ((int64_t)b * p.nq + head) * p.sq;
+      lse_st = qr < p.sq ? p.lse[rb + qr] : 0.f;
+      dl_st = qr < p.sq ? P.delta[rb + qr] : 0.f;
+    }
+  };
+  if (nsteps > 0) prefetch(0);
 
-    for (int q0 = q_first; q0 < p.sq; q0 += BQ) {
+  for (int step = 0; step < nsteps; ++step) {
+    const int hh = step / nsteps_q;
+    const int q0 = q_first + (step - hh * nsteps_q) * BQ;
+    const int head = g * r + hh;
+    float* DQ = P.dq_acc + ((int64_t)b * p.nq + head) * (int64_t)p.sq * HD;
+    {
       __syncthreads();  // previous step finished reading LDS
 #pragma unroll
       for (int i = 0; i < QCH; ++i) {
-        const int idx = tid + 256 * i;
-        const int which = idx / (BQ * CPR);  // 0: Q, 1: dO
-        const int rem = idx % (BQ * CPR);
+        const bool is_do = i >= QCH / 2;
+        const int rem = tid + 256 * (i - (is_do ? QCH / 2 : 0));
         const int row = rem / CPR, ch = rem % CPR;
-        int qr = q0 + row;
-        qr = qr < p.sq ? qr : p.sq - 1;
-        if (which == 0)
-          *reinterpret_cast<x8*>(q_lds + sw_off<HD>(row, ch * 8)) =
-              ld8(Q + (int64_t)qr * p.q_ss + ch * 8);
-        else
-          *reinterpret_cast<x8*>(do_lds + sw_off<HD>(row, ch * 8)) =
-              ld8(DO + (int64_t)qr * p.o_ss + ch * 8);
+        *reinterpret_cast<x8*>((is_do ? do_lds : q_lds) + sw_off<HD>(row, ch * 8)) = qst[i];
       }
       if (tid < BQ) {
-        const int qr = q0 + tid;
-        lse_lds[tid] = qr < p.sq ? LSE[qr] : 0.f;
-        dl_lds[tid] = qr < p.sq ? DL[qr] : 0.f;
+        lse_lds[tid] = lse_st;
+        dl_lds[tid] = dl_st;
       }
+      if (step + 1 < nsteps) prefetch(step + 1);
       __syncthreads();
 
       f32x16 sacc, dpacc;

@@ -67,15 +67,32 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_k(const AttnParams p) {
 
   // staging registers: KCH chunks of K and of V for the next tile
   x8 kst[KCH], vst[KCH];
-  auto load_tile = [&](int n0) {
+  // per-thread element offsets of its staged chunks (row i*256/CPR + tid/CPR)
+  int krow[KCH];
+  int64_t koff[KCH], voff[KCH];
 #pragma unroll
-    for (int i = 0; i < KCH; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / CPR, ch = idx % CPR;
-      int key = n0 + row;
-      key = key < p.sk ? key : p.sk - 1;
-      kst[i] = ld8(K + (int64_t)key * p.k_ss + ch * 8);
-      vst[i] = ld8(V + (int64_t)key * p.v_ss + ch * 8);
+  for (int i = 0; i < KCH; ++i) {
+    const int idx = tid + 256 * i;
+    krow[i] = idx / CPR;
+    koff[i] = (int64_t)krow[i] * p.k_ss + (idx % CPR) * 8;
+    voff[i] = (int64_t)krow[i] * p.v_ss + (idx % CPR) * 8;
+  }
+  auto load_tile = [&](int n0) {
+    const T* kt = K + (int64_t)n0 * p.k_ss;  // wave-uniform tile bases (SALU)
+    const T* vt = V + (int64_t)n0 * p.v_ss;
+    if (n0 + BN <= p.sk) {
+#pragma unroll
+      for (int i = 0; i < KCH; ++i) {
+        kst[i] = ld8(kt + koff[i]);
+        vst[i] = ld8(vt + voff[i]);
+      }
+    } else {  // ragged last tile: clamp keys (masked later)
+#pragma unroll
+      for (int i = 0; i < KCH; ++i) {
+        const int64_t back = (n0 + krow[i] < p.sk) ? 0 : (int64_t)(n0 + krow[i] - (p.sk - 1));
+        kst[i] = ld8(kt + koff[i] - back * p.k_ss);
+        vst[i] = ld8(vt + voff[i] - back * p.v_ss);
+      }
     }
   };
   auto store_tile = [&]() {
@@ -118,13 +135,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_k(const AttnParams p) {
       s0 = MT<T>::mfma(ka0, qf[kk], s0);
       s1 = MT<T>::mfma(ka1, qf[kk], s1);
     }
-    // scale (log2 domain) + mask
+    // mask (raw scores; the log2-domain scale is fused into the exp argument)
     const bool need_mask = CAUSAL ? (n0 + BN - 1 > m0 + off) : (n0 + BN > p.sk);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s0[i] *= sl2;
-      s1[i] *= sl2;
-    }
     if (need_mask) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -138,27 +150,38 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_k(const AttnParams p) {
         if (!ok1) s1[i] = -INFINITY;
       }
     }
+    // Online softmax in the log2 domain.  m_i is kept in SCALED units
+    // (max(s) * scale * log2 e, scale > 0), so p = exp2(fma(s, sl2, -m)):
+    // one FMA + one raw v_exp_f32 per score (exp2f would add a denormal
+    // range-reduction sequence; outputs < 2^-126 are irrelevant here).
     float mt = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    for (int i = 0; i < 16; i += 2)
+      mt = fmaxf(mt, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
     const float m_new = fmaxf(m_i, mt);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_i - m_use);
-    float rs = 0.f;
+    const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
+    float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      s0[i] = exp2f(s0[i] - m_use);
-      s1[i] = exp2f(s1[i] - m_use);
-      rs += s0[i] + s1[i];
+      s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sl2, -m_use));
+      s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sl2, -m_use));
+      rs0 += s0[i];
+      rs1 += s1[i];
     }
+    float rs = rs0 + rs1;
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
     m_i = m_new;
+    // The running max rarely moves once a row has seen its largest scores:
+    // skip the O rescale when no lane of the wave needs it (wave-uniform).
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-    for (int d = 0; d < DT; ++d)
+      for (int d = 0; d < DT; ++d)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+    }
 
     // O^T[d][q] += V^T[d][key] * P^T[key][q]
 #pragma unroll

@@ -10,9 +10,9 @@ MI355X-specific design of the GEMM path (``_LinearFn``):
 * Forward, dgrad and wgrad GEMMs run on hipBLASLt through PyTorch
   (``EMA_GEMM=tuned`` switches to ``ops/gemm.py``'s per-shape solution
   timing; ``EMA_WGRAD=hip`` to the hand-written MFMA wgrad kernel).
-* With ``gradient_accumulation_fusion`` the weight gradient is produced by the
-  hand-written gfx950 MFMA kernel ``csrc/gemm_wgrad.hip`` (bf16 x bf16 -> fp32)
-  written **in place** into the fp32 ``main_grad`` view of the DDP bucket —
+* With ``gradient_accumulation_fusion`` the weight gradient is a
+  bf16 x bf16 -> fp32 GEMM written **in place** into the fp32 ``main_grad``
+  view of the DDP bucket —
   no separate wgrad tensor, no accumulate kernel, and no zero-fill (the first
   micro-batch stores with beta = 0; reference N8 / apex
   ``fused_weight_gradient_mlp_cuda``).  Immediately after
