@@ -135,8 +135,8 @@ class NullTokenizer(AbstractTokenizer):
 class GPT2BPETokenizer(AbstractTokenizer):
     def __init__(self, vocab_file, merge_file):
         super().__init__("GPT2 BPE")
-        from transformers import GPT2Tokenizer
-        self.tokenizer = GPT2Tokenizer(vocab_file, merge_file, errors="replace")
+        from .gpt2_bpe import GPT2BPE
+        self.tokenizer = GPT2BPE(vocab_file, merge_file, errors="replace")
         self.eod_id = self.tokenizer.encoder["<|endoftext|>"]
 
     @property

@@ -1,0 +1,365 @@
+"""Unit tests mirroring the reference's tests/ (test_utils, test_activations,
+tensor_parallel/test_{mappings,cross_entropy,random,data,tensor_parallel_utils})
+plus scheduler / grad scaler / microbatch / checkpoint-resume coverage.
+Multi-rank cases run on gloo (the reference needed 8 GPUs for these)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from dist_utils import run_dist, init_framework, TINY_LLAMA
+
+
+# ----------------------------------------------------------------- core utils
+def test_divide():
+    from epfl_megatron_amd.parallel.buffers import divide
+    assert divide(4, 2) == 2
+    with pytest.raises(AssertionError):
+        divide(4, 5)
+
+
+def test_global_memory_buffer_and_viewless():
+    from epfl_megatron_amd.parallel.buffers import (GlobalMemoryBuffer, assert_viewless_tensor,
+                                                    make_viewless_tensor,
+                                                    safely_set_viewless_tensor_data)
+    buf = GlobalMemoryBuffer()
+    t = buf.get_tensor((3, 2), torch.float32, "t")
+    assert t.shape == (3, 2)
+    t2 = buf.get_tensor((2, 2), torch.float32, "t")  # reuses the same storage
+    assert t2.data_ptr() == t.data_ptr()
+    inp = torch.rand(3, 4)
+    for keep in (True, False):
+        out = make_viewless_tensor(inp, True, keep)
+        assert torch.equal(out, inp) and out._base is None
+    z = torch.zeros(3, 4)
+    new = torch.rand(3, 4)
+    safely_set_viewless_tensor_data(z, new)
+    assert torch.equal(z, new)
+    assert torch.equal(assert_viewless_tensor(new), new)
+    assert all(torch.equal(a, b) for a, b in zip(assert_viewless_tensor([new, new]), [new, new]))
+
+
+def test_tensor_parallel_utils_single():
+    from epfl_megatron_amd.parallel.tensor.utils import VocabUtility, split_tensor_along_last_dim
+    x = torch.arange(24.0).view(2, 12)
+    parts = split_tensor_along_last_dim(x, 3)
+    assert [p.shape for p in parts] == [(2, 4)] * 3 and torch.equal(torch.cat(parts, -1), x)
+    assert VocabUtility.vocab_range_from_global_vocab_size(100, 2, 4) == (50, 75)
+    assert VocabUtility.vocab_range_from_per_partition_vocab_size(25, 1, 4) == (25, 50)
+
+
+# ----------------------------------------------------------------- activations
+@pytest.mark.parametrize("kind,act", [("swiglu", F.silu), ("geglu", F.gelu), ("reglu", F.relu),
+                                      ("liglu", lambda t: t)])
+def test_glu_family(kind, act):
+    from epfl_megatron_amd.ops.activations import GLU_ACTIVATIONS
+    torch.manual_seed(11)
+    x = torch.randn(3, 17, 2 * 48)
+    x1, x2 = x.chunk(2, dim=-1)
+    out = GLU_ACTIVATIONS[kind](x)
+    assert out.shape == (3, 17, 48)
+    # first half "up", second half gated (reference glu_activations.py:18-21)
+    torch.testing.assert_close(out, x1 * act(x2), atol=1e-5, rtol=1e-5)
+
+
+def test_bias_gelu_and_gelu():
+    from epfl_megatron_amd.ops.activations import bias_gelu, gelu
+    torch.manual_seed(0)
+    y = torch.randn(5, 8, requires_grad=True)
+    b = torch.randn(8, requires_grad=True)
+    out = bias_gelu(b, y)
+    ref = F.gelu(y + b, approximate="tanh")
+    torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+    out.sum().backward()
+    y2, b2 = y.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    F.gelu(y2 + b2, approximate="tanh").sum().backward()
+    torch.testing.assert_close(y.grad, y2.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(b.grad, b2.grad, atol=1e-5, rtol=1e-5)
+    x = torch.randn(7)
+    torch.testing.assert_close(gelu(x), F.gelu(x), atol=1e-6, rtol=1e-6)
+
+
+# --------------------------------------------------------- multi-rank (gloo)
+def _init_mp(rank, world, tp, pp):
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from epfl_megatron_amd.parallel import state
+    state.initialize_model_parallel(tp, pp)
+    return state
+
+
+def _mappings(rank, world):
+    state = _init_mp(rank, world, 4, 2)
+    from epfl_megatron_amd.parallel.tensor import mappings as m
+    out = {}
+    x = torch.ones(1) * rank
+    out["reduce"] = m.reduce_from_tensor_model_parallel_region(x.clone()).item()
+    inp = torch.arange(32.0).view(8, 4)
+    out["scatter_last"] = m.scatter_to_tensor_model_parallel_region(inp).flatten().tolist()
+    out["gather_last"] = m.gather_from_tensor_model_parallel_region(
+        torch.ones(8, 1) * rank).tolist()
+    out["scatter_seq"] = m.scatter_to_sequence_parallel_region(inp).tolist()
+    out["gather_seq"] = m.gather_from_sequence_parallel_region(torch.ones(2, 4) * rank).tolist()
+    out["rs_seq"] = m.reduce_scatter_to_sequence_parallel_region(
+        torch.ones(8, 4) * rank).tolist()
+    # backward of copy = all-reduce
+    y = torch.ones(3, requires_grad=True)
+    m.copy_to_tensor_model_parallel_region(y).backward(torch.ones(3) * rank)
+    out["copy_bwd"] = y.grad.tolist()
+    state.destroy_model_parallel()
+    return out
+
+
+def test_mappings_tp4_pp2():
+    res = run_dist(_mappings, 8)
+    for rank, r in enumerate(res):
+        tp_rank = rank % 4
+        group_sum = sum(range(4 * (rank // 4), 4 * (rank // 4) + 4))
+        assert r["reduce"] == group_sum
+        inp = torch.arange(32.0).view(8, 4)
+        assert r["scatter_last"] == inp[:, tp_rank].tolist()
+        base = 4 * (rank // 4)
+        assert r["gather_last"] == [[float(base + i) for i in range(4)]] * 8
+        assert r["scatter_seq"] == inp[2 * tp_rank:2 * tp_rank + 2].tolist()
+        assert r["gather_seq"] == [[float(base + i)] * 4 for i in range(4) for _ in range(2)]
+        assert r["rs_seq"] == [[float(group_sum)] * 4] * 2
+        assert r["copy_bwd"] == [float(group_sum)] * 3
+
+
+def _tp_utils(rank, world):
+    state = _init_mp(rank, world, 2, 1)
+    from epfl_megatron_amd.parallel.tensor.utils import (gather_split_1d_tensor,
+                                                         split_tensor_into_1d_equal_chunks)
+    x = torch.arange(12.0).view(3, 4)
+    part = split_tensor_into_1d_equal_chunks(x)
+    full = gather_split_1d_tensor(part)
+    state.destroy_model_parallel()
+    return part.tolist(), full.view(3, 4).tolist()
+
+
+def test_split_gather_1d():
+    res = run_dist(_tp_utils, 2)
+    assert res[0][0] == list(range(6)) and res[1][0] == list(range(6, 12))
+    assert res[0][1] == torch.arange(12.0).view(3, 4).tolist()
+
+
+def _vocab_ce(rank, world, smoothing):
+    state = _init_mp(rank, world, 2, 1)
+    from epfl_megatron_amd.ops.cross_entropy import vocab_parallel_cross_entropy
+    torch.manual_seed(0)
+    logits = torch.randn(5, 3, 16)
+    target = torch.randint(0, 16, (5, 3))
+    mine = logits[..., rank * 8:(rank + 1) * 8].clone().requires_grad_()
+    loss = vocab_parallel_cross_entropy(mine, target, label_smoothing=smoothing)
+    loss.sum().backward()
+    state.destroy_model_parallel()
+    return loss.detach(), mine.grad, logits, target
+
+
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_vocab_parallel_cross_entropy(smoothing):
+    res = run_dist(_vocab_ce, 2, smoothing)
+    logits, target = res[0][2].requires_grad_(), res[0][3]
+    # reference smoothing (megatron/core/tensor_parallel/cross_entropy.py:71-87):
+    # alpha' = alpha * K / (K - 1); loss = (1 - alpha') * nll - alpha' * mean(log p)
+    logp = F.log_softmax(logits, dim=-1)
+    nll = -logp.gather(-1, target.unsqueeze(-1)).squeeze(-1)
+    a = smoothing * 16 / 15
+    ref = (1 - a) * nll - a * logp.mean(-1)
+    ref.sum().backward()
+    for rank, (loss, grad, _, _) in enumerate(res):
+        torch.testing.assert_close(loss, ref.detach(), atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(grad, logits.grad[..., rank * 8:(rank + 1) * 8],
+                                   atol=1e-5, rtol=1e-5)
+
+
+def _broadcast(rank, world):
+    state = _init_mp(rank, world, 2, 1)
+    from epfl_megatron_amd.parallel.tensor.data import broadcast_data
+    data = None
+    if rank % 2 == 0:
+        data = {"text": torch.arange(12).view(3, 4) + rank, "mask": torch.ones(2, 2)}
+    out = broadcast_data(["text"], data, torch.int64)
+    state.destroy_model_parallel()
+    return out["text"].tolist()
+
+
+def test_broadcast_data_over_tp():
+    res = run_dist(_broadcast, 4)
+    assert res[0] == res[1] == (torch.arange(12).view(3, 4)).tolist()
+    assert res[2] == res[3] == (torch.arange(12).view(3, 4) + 2).tolist()
+
+
+def _rng(rank, world):
+    state = _init_mp(rank, world, 2, 1)
+    from epfl_megatron_amd.parallel.tensor.random import (get_cuda_rng_tracker,
+                                                          model_parallel_cuda_manual_seed)
+    model_parallel_cuda_manual_seed(123)
+    tracker = get_cuda_rng_tracker()
+    with tracker.fork():
+        a = torch.rand(4)
+    b = torch.rand(4)  # default stream: same across TP ranks
+    states = tracker.get_states()
+    with tracker.fork():
+        a2 = torch.rand(4)
+    tracker.set_states(states)
+    with tracker.fork():
+        a3 = torch.rand(4)
+    state.destroy_model_parallel()
+    return a.tolist(), b.tolist(), a2.tolist(), a3.tolist()
+
+
+def test_rng_tracker_tp():
+    res = run_dist(_rng, 2)
+    (a0, b0, a20, a30), (a1, b1, _, _) = res
+    assert a0 != a1          # model-parallel stream differs per TP rank
+    assert b0 == b1          # default stream identical
+    assert a20 == a30        # set_states restores the fork's stream
+
+
+def test_checkpoint_function_recompute_matches():
+    from epfl_megatron_amd.parallel.tensor.random import checkpoint
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(8, 8)
+    x = torch.randn(4, 8, requires_grad=True)
+
+    def fn(t):
+        return F.dropout(torch.tanh(lin(t)), p=0.0) * 2
+
+    y = checkpoint(fn, False, x)
+    y.sum().backward()
+    g1 = x.grad.clone()
+    x.grad = None
+    fn(x).sum().backward()
+    torch.testing.assert_close(g1, x.grad)
+
+
+# ------------------------------------------------------- schedules / scalers
+class _Opt:
+    def __init__(self):
+        self.param_groups = [{"lr": 0.0, "weight_decay": 0.0}]
+
+
+def test_lr_schedules():
+    from epfl_megatron_amd.optim.scheduler import OptimizerParamScheduler
+    for style in ("linear", "cosine", "constant", "inverse-square-root"):
+        s = OptimizerParamScheduler(_Opt(), 1.0, 0.1, 10, 110, style, 0.0, 0.1, 100, "linear")
+        lrs = []
+        for _ in range(120):
+            s.step(1)
+            lrs.append(s.get_lr())
+        assert lrs[4] == pytest.approx(0.5)       # warmup: 5/10
+        if style == "linear":
+            assert lrs[59] == pytest.approx(1.0 - 0.9 * 50 / 100)
+            assert lrs[-1] == pytest.approx(0.1)
+        if style == "cosine":
+            assert lrs[59] == pytest.approx(0.1 + 0.9 * 0.5 * (math.cos(math.pi * 0.5) + 1))
+            assert lrs[109] == pytest.approx(0.1)
+        if style == "constant":
+            assert lrs[50] == 1.0
+        if style == "inverse-square-root":
+            assert lrs[39] == pytest.approx(max(0.1, math.sqrt(10) / math.sqrt(40)))
+        assert s.get_wd() == pytest.approx(0.1)
+    s = OptimizerParamScheduler(_Opt(), 1.0, 0.0, 0, 100, "linear", 0.0, 0.1, 100, "cosine")
+    s.step(50)
+    assert s.get_wd() == pytest.approx(0.05)
+    sd = s.state_dict()
+    s2 = OptimizerParamScheduler(_Opt(), 1.0, 0.0, 0, 100, "linear", 0.0, 0.1, 100, "cosine")
+    s2.load_state_dict(sd)
+    assert s2.num_steps == 50 and s2.get_lr() == pytest.approx(s.get_lr())
+
+
+def test_dynamic_grad_scaler():
+    from epfl_megatron_amd.optim.grad_scaler import ConstantGradScaler, DynamicGradScaler
+    s = DynamicGradScaler(2.0 ** 16, 1.0, 2.0, 0.5, 3, 2)
+    s.update(True)
+    assert s.scale.item() == 2.0 ** 16        # hysteresis 2: first inf tolerated
+    s.update(True)
+    assert s.scale.item() == 2.0 ** 15
+    for _ in range(3):
+        s.update(False)
+    assert s.scale.item() == 2.0 ** 16
+    s2 = DynamicGradScaler(4.0, 1.0, 2.0, 0.5, 3, 1)
+    s2.load_state_dict(s.state_dict())
+    assert s2.scale.item() == 2.0 ** 16
+    for _ in range(40):
+        s2.update(True)
+    assert s2.scale.item() == 1.0             # min_scale floor
+    c = ConstantGradScaler(8.0)
+    c.update(True)
+    assert c.scale.item() == 8.0 and c.inv_scale.item() == 0.125
+
+
+def test_microbatch_calculators():
+    from epfl_megatron_amd.config.microbatches import (ConstantNumMicroBatches,
+                                                       RampupBatchsizeNumMicroBatches)
+    c = ConstantNumMicroBatches(64, 4, 2)
+    assert c.get() == 8 and c.get_current_global_batch_size() == 64
+    with pytest.raises(AssertionError):
+        ConstantNumMicroBatches(63, 4, 2)
+    r = RampupBatchsizeNumMicroBatches(16, 16, 1000, 64, 4, 2)
+    assert r.get_current_global_batch_size() == 16 and r.get() == 2
+    r.update(500, True)
+    assert r.get_current_global_batch_size() == 32  # 16 + 16 * int(500 / (1000 / 3))
+    r.update(2000, True)
+    assert r.get_current_global_batch_size() == 64 and r.get() == 8
+
+
+# ------------------------------------------------------------- arguments
+def test_validate_args_derivations():
+    from epfl_megatron_amd.config.arguments import parse_args, validate_args
+    args = parse_args(None, ["--num_layers", "4", "--hidden_size", "64",
+                             "--num_attention_heads", "8", "--seq_length", "32",
+                             "--max_position_embeddings", "32", "--micro_batch_size", "2",
+                             "--bf16", "--tensor_model_parallel_size", "1"])
+    args.rank, args.world_size = 0, 4
+    validate_args(args, {})
+    assert args.data_parallel_size == 4
+    assert args.ffn_hidden_size == 256 and args.kv_channels == 8
+    assert args.num_attention_heads_kv == 8
+    assert args.params_dtype == torch.bfloat16
+    assert args.accumulate_allreduce_grads_in_fp32
+    assert args.global_batch_size == 8  # micro x dp default
+    assert not args.sequence_parallel
+
+
+# ------------------------------------------------------ checkpoint / resume
+def _train_save_resume(rank, world, ckdir, phase):
+    import finetune
+    argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "2",
+                         "--save", ckdir, "--save_interval", "2"]
+    if phase == "resume":
+        argv += ["--load", ckdir]
+    argv[argv.index("--train_iters") + 1] = "4"
+    if phase == "first":  # interrupted run: checkpoint + exit at iteration 2
+        argv += ["--exit_interval", "2"]
+    init_framework(argv, finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.training import pretrain
+    args = get_args()
+    try:
+        model, opt, sched = pretrain(args, finetune.train_valid_test_datasets_provider,
+                                     finetune.model_provider, ModelType.encoder_or_decoder,
+                                     finetune.forward_step)
+    except SystemExit:
+        return "exited", args.iteration
+
+    from epfl_megatron_amd.utils.misc import unwrap_model
+    w = unwrap_model(model)[0].language_model.encoder.layers[0].self_attention.dense.weight
+    return args.iteration, args.consumed_train_samples, w.detach().float().clone(), \
+        sched.num_steps
+
+
+def test_checkpoint_resume_matches_uninterrupted(tmp_path):
+    straight = run_dist(_train_save_resume, 2, str(tmp_path / "a"), "full")
+    first = run_dist(_train_save_resume, 2, str(tmp_path / "b"), "first")
+    assert [f[0] for f in first] == ["exited"] * 2
+    assert (tmp_path / "b" / "latest_checkpointed_iteration.txt").read_text() == "2"
+    resumed = run_dist(_train_save_resume, 2, str(tmp_path / "b"), "resume")
+    for s, r in zip(straight, resumed):
+        assert s[1] == r[1] == 8 and s[3] == r[3] == 8  # samples consumed / scheduled
+        torch.testing.assert_close(s[2], r[2], atol=1e-6, rtol=1e-6)
+    assert (tmp_path / "b" / "latest_checkpointed_iteration.txt").read_text() == "4"
