@@ -225,3 +225,26 @@ def test_falcon_hf_logit_parity(tmp_path, new_arch):
                       str(tmp_path / "back"), "--model", "falcon", "--no_tokenizer"])
     back = transformers.FalconForCausalLM.from_pretrained(str(tmp_path / "back")).float().eval()
     torch.testing.assert_close(_hf_logits(back, tokens), want)
+
+
+def _verify(rank, world, ckpt, hfdir):
+    import verify_correctness as vc
+    from dist_utils import init_framework
+    argv = ["--model_name", "llama2", "--load", ckpt, "--huggingface_cache", hfdir,
+            "--huggingface_device", "cpu", "--synthetic_data", "--tokenizer_type",
+            "NullTokenizer", "--synthetic_vocab_size", "96", "--make_vocab_size_divisible_by",
+            "1", "--seq_length", "16", "--use_cpu_initialization", "--global_batch_size", "1",
+            "--no_bias_gelu_fusion", "--no_bias_dropout_fusion", "--hidden_dropout", "0.0",
+            "--attention_dropout", "0.0", "--eval_iters", "0"]
+    from epfl_megatron_amd.initialize import initialize_megatron
+    initialize_megatron(vc.extra_extra_args, vc.defaults_for(ckpt),
+                        args_list=["--distributed_backend", "gloo", "--num_workers", "0"] + argv)
+    return vc.main(iters=2)
+
+
+def test_verify_correctness_cli(llama_ckpt):
+    d, _, _ = llama_ckpt
+    res = run_dist(_verify, 1, str(d / "mega"), str(d / "hf"))[0]
+    assert len(res) == 2
+    for max_err, loss_err in res:
+        assert max_err < 1e-3 and loss_err < 1e-4
