@@ -7,7 +7,8 @@
 ``beam_width``, ``stop_token``, ``length_penalty``) answering
 ``{"text", "segments", "logprobs"}`` or ``{"text", "segments", "scores"}``.
 
-Flask is not part of this image, so the app is FastAPI/uvicorn.  Validation
+Flask is not part of this image, so the app is FastAPI/uvicorn; ``GET /``
+serves the small web UI in ``static/index.html`` (reference ``megatron/static``).  Validation
 lives in :func:`parse_request` (pure, unit-tested); invalid requests get HTTP
 400 with the reference's message (the reference answered some of them with
 200).  Rank 0 serves; before each request it broadcasts a command code
@@ -16,6 +17,7 @@ lives in :func:`parse_request` (pure, unit-tested); invalid requests get HTTP
 """
 import datetime
 import json
+import os
 import threading
 
 import torch
@@ -178,6 +180,9 @@ def stop_workers():
     _send_choice(STOP_NUM)
 
 
+_INDEX_HTML = os.path.join(os.path.dirname(os.path.abspath(__file__)), "static", "index.html")
+
+
 class MegatronServer:
 
     def __init__(self, model):
@@ -185,6 +190,12 @@ class MegatronServer:
         from fastapi.responses import JSONResponse, PlainTextResponse
         self.app = FastAPI()
         self.model = model
+
+        @self.app.get("/")
+        def index():
+            from fastapi.responses import HTMLResponse
+            with open(_INDEX_HTML, encoding="utf-8") as f:
+                return HTMLResponse(f.read())
 
         @self.app.put("/api")
         def api(body: dict, request: Request):  # sync handler -> worker thread

@@ -248,3 +248,42 @@ def test_verify_correctness_cli(llama_ckpt):
     assert len(res) == 2
     for max_err, loss_err in res:
         assert max_err < 1e-3 and loss_err < 1e-4
+
+
+def _hf_to_meta_layout(w, n_heads):
+    """HF rotate-half rows -> Meta interleaved rows (inverse of HF's own permute)."""
+    hd = w.shape[0] // n_heads
+    return w.view(n_heads, 2, hd // 2, w.shape[1]).transpose(1, 2).reshape(w.shape)
+
+
+def test_convert_llama2hf_from_meta_shards(llama_ckpt, tmp_path):
+    """Tiny HF model -> genuine 2-way Meta shards -> convert_llama2hf -> same HF weights."""
+    import json
+    import convert_llama2hf
+    from epfl_megatron_amd.convert.llama import META_SHARD_DIM, hf_to_meta
+    d, hf, tokens = llama_ckpt
+    meta = hf_to_meta(hf.state_dict())
+    for k in list(meta):
+        if k.endswith("attention.wq.weight"):
+            meta[k] = _hf_to_meta_layout(meta[k], 4)
+        elif k.endswith("attention.wk.weight"):
+            meta[k] = _hf_to_meta_layout(meta[k], 2)
+    src = tmp_path / "meta" / "7B"
+    src.mkdir(parents=True)
+    for r in range(2):
+        shard = {}
+        for k, v in meta.items():
+            dim = META_SHARD_DIM[k.split(".")[-2]]
+            shard[k] = v.clone() if dim is None else torch.chunk(v, 2, dim=dim)[r].clone()
+        torch.save(shard, src / f"consolidated.{r:02d}.pth")
+    (src / "params.json").write_text(json.dumps({"dim": 64, "n_layers": 4, "n_heads": 4,
+                                                 "n_kv_heads": 2, "norm_eps": 1e-5,
+                                                 "vocab_size": 96}))
+    out = tmp_path / "hf_out"
+    convert_llama2hf.main(["--input_dir", str(tmp_path / "meta"), "--model_size", "7B",
+                           "--output_dir", str(out)])
+    back = transformers.LlamaForCausalLM.from_pretrained(str(out)).float().eval()
+    ref = hf.state_dict()
+    for k, v in back.state_dict().items():
+        assert torch.equal(v, ref[k]), k
+    torch.testing.assert_close(_hf_logits(back, tokens), _hf_logits(hf, tokens))

@@ -165,6 +165,8 @@ def _rest(rank, world):
     bad = client.put("/api", json={"prompts": "x"})
     beam = client.put("/api", json={"prompts": ["3 14"], "tokens_to_generate": 2,
                                     "beam_width": 2, "stop_token": 249, "no_log": True})
+    page = client.get("/")
+    assert page.status_code == 200 and 'fetch("/api"' in page.text
     return ok.status_code, ok.json(), bad.status_code, bad.text, beam.status_code, beam.json()
 
 
