@@ -445,9 +445,7 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   p.dq = dq.data_ptr();
   p.dk = dk.data_ptr();
   p.dv = dv.data_ptr();
-  auto dq_acc = at::empty({b * nq * sq * hd}, q.options().dtype(at::kFloat));
   auto delta = at::empty({b * nq * sq}, q.options().dtype(at::kFloat));
-  p.dq_acc = dq_acc.data_ptr<float>();
   p.delta = delta.data_ptr<float>();
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }

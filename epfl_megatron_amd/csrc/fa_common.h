@@ -46,6 +46,56 @@ struct MT<fp16> {
   }
 };
 
+// Inline-asm MFMAs with the accumulator's register class pinned: "+a" for
+// loop-carried accumulators that only ever feed further MFMAs (dK/dV/dQ),
+// "+v" for short-lived ones read by VALU right after (S, dP).  Left to the
+// register allocator, a 1-wave/SIMD kernel with saturated arch VGPRs gets
+// its accumulators shuttled AGPR <-> VGPR around every MFMA.
+// hipcc pads no hazard inside an asm string (CDNA guide §5.7):
+//   * NOP = 1: an operand (A, B or C) was just written by VALU -> s_nop 1;
+//   * back-to-back MFMAs accumulating into the same registers need nothing;
+//   * VALU / stores reading an MFMA result need 18 wait states: mfma_drain().
+template <typename T, int NOP = 0>
+__device__ __forceinline__ void mfma_agpr(f32x16& acc, typename MT<T>::x8 a,
+                                          typename MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16)) {
+    if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  } else {
+    if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    else asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  }
+}
+template <typename T, int NOP = 0>
+__device__ __forceinline__ void mfma_vgpr(f32x16& acc, typename MT<T>::x8 a,
+                                          typename MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16)) {
+    if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  } else {
+    if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    else asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  }
+}
+// acc = A * B (C = 0), VGPR destination
+template <typename T>
+__device__ __forceinline__ f32x16 mfma_vgpr0(typename MT<T>::x8 a, typename MT<T>::x8 b) {
+  f32x16 acc;
+  if constexpr (__is_same(T, bf16))
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+
+// Wait states between an asm MFMA and any VALU / store reading its result
+// (16-pass XDL op: 18 states, padded to 24).
+__device__ __forceinline__ void mfma_drain() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <typename T>
 __device__ __forceinline__ typename MT<T>::x8 ld8(const T* p) {
   return *reinterpret_cast<const typename MT<T>::x8*>(p);

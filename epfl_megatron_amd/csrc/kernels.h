@@ -90,8 +90,9 @@ struct AttnBwdParams {
   void* dq;  // same strides as q
   void* dk;  // same strides as k
   void* dv;  // same strides as v
-  float* dq_acc;  // fp32 [b, nq, sq, hd] workspace (zeroed by the launcher)
   float* delta;   // fp32 [b, nq, sq] workspace
+  int ablate;     // profiling only (EMA_FA_ABLATE): bit 0 = no in-loop global prefetch
+  uint64_t* stamps;  // diagnostic build only (EMA_FA_STAMPS)
 };
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);

@@ -42,6 +42,8 @@ def main():
         G = torch.zeros(N, K, device="cuda", dtype=torch.float32)
         Gt = torch.zeros(K, N, device="cuda", dtype=torch.float32)
         fl = 2.0 * M * N * K
+        dYt = dY.t().contiguous()
+        Xt = X.t().contiguous()
         forms = {
             "fwd_matmul_WT": lambda: torch.matmul(X, W.t()),
             "fwd_linear": lambda: F.linear(X, W),
@@ -51,6 +53,13 @@ def main():
             "wgrad_addmm_fp32": lambda: torch.addmm(G, dY.t(), X, out_dtype=torch.float32, out=G),
             "wgrad_addmm_fp32_T": lambda: torch.addmm(Gt, X.t(), dY, out_dtype=torch.float32, out=Gt),
             "wgrad_mm_bf16": lambda: torch.mm(dY.t(), X),
+            # token-contiguous (pre-transposed) operands: K-contiguous on both sides
+            "wgrad_TN_fp32": lambda: torch.addmm(G, dYt, Xt.t(), out_dtype=torch.float32, out=G),
+            "wgrad_TN_bf16": lambda: torch.mm(dYt, Xt.t()),
+        }
+        copies = {
+            "transpose_X_us": lambda: X.t().contiguous(),
+            "transpose_dY_us": lambda: dY.t().contiguous(),
         }
         res[name] = {}
         for fname, fn in forms.items():
@@ -59,6 +68,8 @@ def main():
                 res[name][fname] = round(fl / dt / 1e12, 1)
             except Exception as e:  # pragma: no cover
                 res[name][fname] = f"err: {str(e)[:80]}"
+        for cname, fn in copies.items():
+            res[name][cname] = round(bench(fn) * 1e6, 1)
         print(name, json.dumps(res[name]), flush=True)
     if a.out:
         with open(a.out, "w") as f:

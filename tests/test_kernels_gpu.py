@@ -363,3 +363,21 @@ def test_tuned_gemm_products(tmp_path, monkeypatch):
     _close(g, ref, atol=0.05, rtol=1e-3, msg="wgrad store")
     gemm.wgrad(g, dy, x, True)
     _close(g, 2 * ref, atol=0.1, rtol=1e-3, msg="wgrad accumulate")
+
+
+def test_flash_attention_bwd_kv_longer():
+    """Backward with sk > sq (bottom-right causal alignment) and ragged tiles."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    torch.manual_seed(11)
+    q = torch.randn(1, 100, 4, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(1, 230, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(1, 230, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_func(q, k, v, causal=True)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = attention_ref(qr, kr, vr, causal=True)
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float())
+    _close(q.grad, qr.grad, 5e-2, 5e-2, "dq (sk > sq)")
+    _close(k.grad, kr.grad, 5e-2, 5e-2, "dk (sk > sq)")
+    _close(v.grad, vr.grad, 5e-2, 5e-2, "dv (sk > sq)")
