@@ -32,8 +32,8 @@ def _parse(argv=None):
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seq_len", type=int, default=1024)
-    ap.add_argument("--micro_batch", type=int, default=8)
-    ap.add_argument("--num_micro", type=int, default=4, help="micro-batches per GPU per step")
+    ap.add_argument("--micro_batch", type=int, default=16)
+    ap.add_argument("--num_micro", type=int, default=2, help="micro-batches per GPU per step")
     ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
     ap.add_argument("--recompute", default=None, choices=[None, "selective", "full"])
     ap.add_argument("--no_dist_opt", action="store_true")
@@ -171,6 +171,8 @@ def main(argv=None):
             "flops_per_token": fpt,
             "peak_tflops_assumed": args.peak_tflops,
             "final_loss": loss,
+            "max_mem_gb": (round(torch.cuda.max_memory_allocated() / 2**30, 1)
+                           if on_gpu else None),
         }
         print(json.dumps(rec), flush=True)
     dist.barrier()

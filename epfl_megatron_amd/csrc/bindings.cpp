@@ -39,33 +39,55 @@ at::Tensor as_dtype(const at::Tensor& w, const at::Tensor& like) {
 }
 
 // ---------------------------------------------------------------- norms
-std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+// Optional residual: `res` (same shape/dtype as x) -> the norm input is
+// s = x + res, returned as the last output; `dres` -> added into dx.
+at::Tensor check_res(const c10::optional<at::Tensor>& r, const at::Tensor& x, const char* name) {
+  if (!r.has_value() || !r->defined()) return at::Tensor();
+  TORCH_CHECK(r->is_contiguous() && r->sizes() == x.sizes() && r->scalar_type() == x.scalar_type(),
+              name, " must match x (contiguous, same shape and dtype)");
+  check_vec_aligned(*r, name);
+  return *r;
+}
+
+void check_norm_input(const at::Tensor& x, const at::Tensor& w) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [rows, H]");
-  const int64_t rows = x.size(0);
   const int H = (int)x.size(1);
   const int dt = dtype_code(x);
   TORCH_CHECK(H % (16 / x.element_size()) == 0, "hidden size must be a multiple of 16 bytes");
   TORCH_CHECK(H <= ema::norm_max_hidden(dt), "hidden size too large for the norm kernel");
   TORCH_CHECK(w.numel() == H, "weight size mismatch");
   check_vec_aligned(x, "x");
-  auto wc = as_dtype(w, x);
-  auto y = at::empty_like(x);
-  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
-  if (rows > 0)
-    ema::rmsnorm_fwd(x.data_ptr(), wc.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), rows, H,
-                     (float)eps, dt, cur_stream());
-  return {y, rstd};
 }
 
-std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                    const at::Tensor& rstd) {
-  check_gpu(x, "x");
-  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
-  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps,
+                                    const c10::optional<at::Tensor>& res) {
+  check_norm_input(x, w);
   const int64_t rows = x.size(0);
   const int H = (int)x.size(1);
   const int dt = dtype_code(x);
+  auto r = check_res(res, x, "res");
+  auto wc = as_dtype(w, x);
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor sum = r.defined() ? at::empty_like(x) : x;
+  if (rows > 0)
+    ema::rmsnorm_fwd(x.data_ptr(), r.defined() ? r.data_ptr() : nullptr,
+                     r.defined() ? sum.data_ptr() : nullptr, wc.data_ptr(), y.data_ptr(),
+                     rstd.data_ptr<float>(), rows, H, (float)eps, dt, cur_stream());
+  return {y, rstd, sum};
+}
+
+std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
+  check_gpu(x, "x");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
+  TORCH_CHECK(rstd.numel() == x.size(0), "rstd size mismatch");
+  const int64_t rows = x.size(0);
+  const int H = (int)x.size(1);
+  const int dt = dtype_code(x);
+  auto dr = check_res(dres, x, "dres");
   auto wc = as_dtype(w, x);
   auto dx = at::empty_like(x);
   auto dw = at::empty({H}, x.options());
@@ -73,8 +95,8 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   auto part = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     ema::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), rstd.data_ptr<float>(),
-                     dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), rows, H, dt,
-                     cur_stream());
+                     dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
+                     part.data_ptr<float>(), dw.data_ptr(), rows, H, dt, cur_stream());
   } else {
     dw.zero_();
   }
@@ -82,36 +104,44 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
 }
 
 std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w,
-                                      const c10::optional<at::Tensor>& b, double eps) {
-  check_gpu(x, "x");
-  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [rows, H]");
+                                      const c10::optional<at::Tensor>& b, double eps,
+                                      const c10::optional<at::Tensor>& res) {
+  check_norm_input(x, w);
   const int64_t rows = x.size(0);
   const int H = (int)x.size(1);
   const int dt = dtype_code(x);
-  TORCH_CHECK(H % (16 / x.element_size()) == 0, "hidden size must be a multiple of 16 bytes");
-  TORCH_CHECK(H <= ema::norm_max_hidden(dt), "hidden size too large for the norm kernel");
-  TORCH_CHECK(w.numel() == H, "weight size mismatch");
+  auto r = check_res(res, x, "res");
   auto wc = as_dtype(w, x);
   at::Tensor bc;
-  if (b.has_value() && b->defined()) bc = as_dtype(*b, x);
+  if (b.has_value() && b->defined()) {
+    TORCH_CHECK(b->numel() == H, "bias size mismatch");
+    bc = as_dtype(*b, x);
+  }
   auto y = at::empty_like(x);
   auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
   auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor sum = r.defined() ? at::empty_like(x) : x;
   if (rows > 0)
-    ema::layernorm_fwd(x.data_ptr(), wc.data_ptr(), bc.defined() ? bc.data_ptr() : nullptr,
-                       y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H,
-                       (float)eps, dt, cur_stream());
-  return {y, mean, rstd};
+    ema::layernorm_fwd(x.data_ptr(), r.defined() ? r.data_ptr() : nullptr,
+                       r.defined() ? sum.data_ptr() : nullptr, wc.data_ptr(),
+                       bc.defined() ? bc.data_ptr() : nullptr, y.data_ptr(),
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, dt,
+                       cur_stream());
+  return {y, mean, rstd, sum};
 }
 
 std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
                                       const at::Tensor& w, const at::Tensor& mean,
-                                      const at::Tensor& rstd) {
+                                      const at::Tensor& rstd,
+                                      const c10::optional<at::Tensor>& dres) {
   check_gpu(x, "x");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
+  TORCH_CHECK(rstd.numel() == x.size(0) && mean.numel() == x.size(0), "stats size mismatch");
   const int64_t rows = x.size(0);
   const int H = (int)x.size(1);
   const int dt = dtype_code(x);
+  auto dr = check_res(dres, x, "dres");
   auto wc = as_dtype(w, x);
   auto dx = at::empty_like(x);
   auto dw = at::empty({H}, x.options());
@@ -121,9 +151,9 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
   auto pb = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     ema::layernorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), mean.data_ptr<float>(),
-                       rstd.data_ptr<float>(), dx.data_ptr(), pw.data_ptr<float>(),
-                       pb.data_ptr<float>(), dw.data_ptr(), db.data_ptr(), rows, H, dt,
-                       cur_stream());
+                       rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr,
+                       dx.data_ptr(), pw.data_ptr<float>(), pb.data_ptr<float>(), dw.data_ptr(),
+                       db.data_ptr(), rows, H, dt, cur_stream());
   } else {
     dw.zero_();
     db.zero_();
@@ -488,10 +518,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
-  m.def("rmsnorm_fwd", &rmsnorm_fwd);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
-  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"));
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),
+        py::arg("res") = py::none());
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("rstd"),
+        py::arg("dres") = py::none());
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"),
+        py::arg("res") = py::none());
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"),
+        py::arg("mean"), py::arg("rstd"), py::arg("dres") = py::none());
   m.def("rope_qkv_inplace", &rope_qkv_inplace);
   m.def("glu_fwd", &glu_fwd);
   m.def("glu_bwd", &glu_bwd);

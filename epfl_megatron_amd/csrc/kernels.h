@@ -12,15 +12,20 @@ enum DType { DT_F32 = 0, DT_F16 = 1, DT_BF16 = 2 };
 int norm_bwd_partials(int64_t rows);
 int norm_bwd_workspace_rows(int64_t rows);  // rows of the fp32 [*, H] partial workspace
 int norm_max_hidden(int dtype);
-void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
-                 float eps, int dt, hipStream_t s);
-void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                 float* dw_part, void* dw, int64_t rows, int H, int dt, hipStream_t s);
-void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
-                   float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s);
+// res/sum_out (nullable): fused residual add, the norm input is x + res and
+// is also written to sum_out.  dres (nullable): added to dx in backward.
+void rmsnorm_fwd(const void* x, const void* res, void* sum_out, const void* w, void* y,
+                 float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s);
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                 const void* dres, void* dx, float* dw_part, void* dw, int64_t rows, int H,
+                 int dt, hipStream_t s);
+void layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                   void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
+                   hipStream_t s);
 void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
-                   const float* rstd, void* dx, float* dw_part, float* db_part, void* dw,
-                   void* db, int64_t rows, int H, int dt, hipStream_t s);
+                   const float* rstd, const void* dres, void* dx, float* dw_part,
+                   float* db_part, void* dw, void* db, int64_t rows, int H, int dt,
+                   hipStream_t s);
 
 // ---- rope.hip ----------------------------------------------------------------
 // In-place rotation of q (r heads per group) and k (1 head per group) of a

@@ -16,9 +16,18 @@ namespace ema {
 namespace {
 
 constexpr int kWaves = 4;
+// backward grid cap: 2 workgroups (8 waves) per CU; more partial rows cost a
+// little colsum traffic but keep twice the loads in flight.
+constexpr int kBwdBlocks = 512;
+constexpr int kLdsDwMaxH = 4096;  // 4 waves x H x fp32 <= 64 KB of LDS
 
+// res != nullptr: the normalised input is s = x + res (rounded to T, as the
+// reference's bf16 residual add), and s is written to sum_out (the residual
+// stream for the next block) -- one pass instead of an add kernel + a norm.
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
+                                                     const T* __restrict__ res,
+                                                     T* __restrict__ sum_out,
                                                      const T* __restrict__ w, T* __restrict__ y,
                                                      float* __restrict__ rstd_out, int64_t rows,
                                                      int H, float eps) {
@@ -35,6 +44,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
     const int vi = lane + i * 64;
     if (vi < nvec) {
       xv[i] = ld16(xr + vi * N);
+      if (res) {
+        const V16<T> rv = ld16(res + row * H + vi * N);
+#pragma unroll
+        for (int e = 0; e < N; ++e) xv[i].v[e] = from_f<T>(to_f(xv[i].v[e]) + to_f(rv.v[e]));
+        st16(sum_out + row * H + vi * N, xv[i]);
+      }
 #pragma unroll
       for (int e = 0; e < N; ++e) {
         const float f = to_f(xv[i].v[e]);
@@ -63,77 +78,167 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
   }
 }
 
-template <typename T, int VPL, bool DW>
-__global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy,
-                                                     const T* __restrict__ x,
-                                                     const T* __restrict__ w,
-                                                     const float* __restrict__ rstd,
-                                                     T* __restrict__ dx,
-                                                     float* __restrict__ dw_part, int64_t rows,
-                                                     int H) {
+// One wave per row, rows strided by the total wave count; the next row's x/dy
+// are loaded before the current row is reduced (software pipeline), so HBM
+// requests stay in flight across the wave_sum / store phase.  DRES adds the
+// gradient of the residual branch (ds from the next block) into dx:
+// dx = rmsnorm'(dy) + dres, saving the separate autograd add kernel.
+//
+// vmcnt discipline (gfx9 counts loads AND stores in one in-order counter):
+// every global access of an iteration is unconditional and issued in the order
+// [x,dy(row + nwaves)] [dres(row)] [dx stores(row)], and w / dW live in LDS, so
+// phase 1 of a row never waits on the prefetch of the next one.
+template <typename T, int VPL>
+struct RowRegs {
+  V16<T> x[VPL], g[VPL];
+};
+
+template <typename T, int VPL, bool FULL>
+__device__ __forceinline__ void load_row(RowRegs<T, VPL>& rr, const T* __restrict__ x,
+                                         const T* __restrict__ dy, int64_t row, int H, int lane,
+                                         int nvec) {
   constexpr int N = V16<T>::N;
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-  const int nvec = H / N;
-  float acc[VPL][N];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i)
-#pragma unroll
-    for (int e = 0; e < N; ++e) acc[i][e] = 0.f;
-  for (int64_t row = gw; row < rows; row += nwaves) {
-    const float r = rstd[row];
-    const T* xr = x + row * H;
-    const T* dyr = dy + row * H;
-    V16<T> xv[VPL], gv[VPL];
-    float dot = 0.f;
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int vi = lane + i * 64;
-      if (vi < nvec) {
-        xv[i] = ld16(xr + vi * N);
-        gv[i] = ld16(dyr + vi * N);
-        const V16<T> wv = ld16(w + vi * N);
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-          const float xh = to_f(xv[i].v[e]) * r;
-          const float g = to_f(gv[i].v[e]);
-          dot += g * to_f(wv.v[e]) * xh;
-          if (DW) acc[i][e] += g * to_f(from_f<T>(xh));
-        }
-      }
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (FULL || vi < nvec) {
+      rr.x[i] = ld16(x + row * H + vi * N);
+      rr.g[i] = ld16(dy + row * H + vi * N);
     }
-    dot = wave_sum(dot) / (float)H;
-    T* dxr = dx + row * H;
+  }
+}
+
+template <typename T, int VPL, bool DW, bool FULL, bool DRES>
+__device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T, VPL>& nxt,
+                                            int64_t nrow, const T* __restrict__ x,
+                                            const T* __restrict__ dy, float* __restrict__ acc,
+                                            const T* __restrict__ w_lds, float r,
+                                            const T* __restrict__ dres, T* __restrict__ dx,
+                                            int64_t row, int H, int lane, int nvec) {
+  constexpr int N = V16<T>::N;
+  load_row<T, VPL, FULL>(nxt, x, dy, nrow, H, lane, nvec);
+  float dot = 0.f;
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int vi = lane + i * 64;
-      if (vi < nvec) {
-        const V16<T> wv = ld16(w + vi * N);
-        V16<T> o;
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (FULL || vi < nvec) {
+      const V16<T> wv = *reinterpret_cast<const V16<T>*>(w_lds + vi * N);
+      float4 a[N / 4];
+      if (DW) {
 #pragma unroll
-        for (int e = 0; e < N; ++e) {
-          const float xh = to_f(xv[i].v[e]) * r;
-          o.v[e] = from_f<T>(r * (to_f(gv[i].v[e]) * to_f(wv.v[e]) - xh * dot));
-        }
-        st16(dxr + vi * N, o);
+        for (int q = 0; q < N / 4; ++q) a[q] = *reinterpret_cast<const float4*>(acc + vi * N + 4 * q);
+      }
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float xh = to_f(rr.x[i].v[e]) * r;
+        const float g = to_f(rr.g[i].v[e]);
+        dot += g * to_f(wv.v[e]) * xh;
+        if (DW) reinterpret_cast<float*>(a)[e] += g * to_f(from_f<T>(xh));
+      }
+      if (DW) {
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) *reinterpret_cast<float4*>(acc + vi * N + 4 * q) = a[q];
       }
     }
   }
+  // dres is fetched only now (its 32 VGPRs would otherwise overlap the phase-1
+  // temporaries and spill); the wait for it also covers the prefetch, which
+  // has had all of phase 1 to land.
+  V16<T> rv[DRES ? VPL : 1];
+  if (DRES) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (FULL || vi < nvec) rv[i] = ld16(dres + row * H + vi * N);
+    }
+  }
+  dot = wave_sum(dot) / (float)H;
+  T* dxr = dx + row * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + i * 64;
+    if (FULL || vi < nvec) {
+      const V16<T> wv = *reinterpret_cast<const V16<T>*>(w_lds + vi * N);
+      V16<T> o;
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float xh = to_f(rr.x[i].v[e]) * r;
+        float v = r * (to_f(rr.g[i].v[e]) * to_f(wv.v[e]) - xh * dot);
+        if (DRES) v += to_f(rv[i].v[e]);
+        o.v[e] = from_f<T>(v);
+      }
+      st16(dxr + vi * N, o);
+    }
+  }
+}
+
+// LDS: w (H x T) then, with DW, one private fp32 dW row per wave (4 x H x 4 B;
+// H <= 4096 -> <= 72 KB per workgroup).  Keeping dW in VGPRs next to the two
+// row buffers pinned the kernel at 1 wave/SIMD.
+template <typename T, int VPL, bool DW, bool FULL, bool DRES>
+__global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __restrict__ dy,
+                                                        const T* __restrict__ x,
+                                                        const T* __restrict__ w,
+                                                        const float* __restrict__ rstd,
+                                                        const T* __restrict__ dres,
+                                                        T* __restrict__ dx,
+                                                        float* __restrict__ dw_part, int64_t rows,
+                                                        int H) {
+  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
+  constexpr int N = V16<T>::N;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform row bookkeeping in SGPRs (rstd[row] becomes a scalar load)
+  const int64_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+  const int nvec = H / N;
+  T* w_lds = reinterpret_cast<T*>(dyn_lds);
+  float* acc = dyn_lds + (H * sizeof(T) + 15) / 16 * 4 + (threadIdx.x >> 6) * H;
+  for (int j = threadIdx.x; j < nvec; j += 256)
+    *reinterpret_cast<V16<T>*>(w_lds + j * N) = ld16(w + j * N);
+  if (DW) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + i * 64;
+      if (FULL || vi < nvec)
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q)
+          *reinterpret_cast<float4*>(acc + vi * N + 4 * q) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __syncthreads();
+  RowRegs<T, VPL> a, b;
+  int64_t row = gw;
+  if (row < rows) load_row<T, VPL, FULL>(a, x, dy, row, H, lane, nvec);
+  // prefetches past the last row re-read row rows-1 (kept unconditional)
+  while (row < rows) {
+    int64_t nrow = row + nwaves;
+    rms_bwd_row<T, VPL, DW, FULL, DRES>(a, b, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
+                                        rstd[row], dres, dx, row, H, lane, nvec);
+    row = nrow;
+    if (row >= rows) break;
+    nrow = row + nwaves;
+    rms_bwd_row<T, VPL, DW, FULL, DRES>(b, a, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
+                                        rstd[row], dres, dx, row, H, lane, nvec);
+    row = nrow;
+  }
   if (!DW) return;
+  // every lane only touches its own slots of acc (same vi mapping as the rows)
   float* part = dw_part + gw * H;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int vi = lane + i * 64;
-    if (vi < nvec) {
+    if (FULL || vi < nvec)
 #pragma unroll
-      for (int e = 0; e < N; ++e) part[vi * N + e] = acc[i][e];
-    }
+      for (int q = 0; q < N / 4; ++q)
+        *reinterpret_cast<float4*>(part + vi * N + 4 * q) =
+            *reinterpret_cast<const float4*>(acc + vi * N + 4 * q);
   }
 }
 
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x,
+                                                       const T* __restrict__ res,
+                                                       T* __restrict__ sum_out,
                                                        const T* __restrict__ w,
                                                        const T* __restrict__ b,
                                                        T* __restrict__ y, float* __restrict__ mean_out,
@@ -152,6 +257,12 @@ __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x,
     const int vi = lane + i * 64;
     if (vi < nvec) {
       xv[i] = ld16(xr + vi * N);
+      if (res) {
+        const V16<T> rv = ld16(res + row * H + vi * N);
+#pragma unroll
+        for (int e = 0; e < N; ++e) xv[i].v[e] = from_f<T>(to_f(xv[i].v[e]) + to_f(rv.v[e]));
+        st16(sum_out + row * H + vi * N, xv[i]);
+      }
 #pragma unroll
       for (int e = 0; e < N; ++e) s += to_f(xv[i].v[e]);
     }
@@ -201,6 +312,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy,
                                                        const T* __restrict__ w,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
+                                                       const T* __restrict__ dres,
                                                        T* __restrict__ dx,
                                                        float* __restrict__ dw_part,
                                                        float* __restrict__ db_part, int64_t rows,
@@ -250,11 +362,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy,
       const int vi = lane + i * 64;
       if (vi < nvec) {
         const V16<T> wv = ld16(w + vi * N);
+        V16<T> rv;
+        if (dres) rv = ld16(dres + row * H + vi * N);
         V16<T> o;
 #pragma unroll
         for (int e = 0; e < N; ++e) {
           const float xh = (to_f(xv[i].v[e]) - mu) * r;
-          o.v[e] = from_f<T>(r * (to_f(gv[i].v[e]) * to_f(wv.v[e]) - sg - xh * sgx));
+          float v = r * (to_f(gv[i].v[e]) * to_f(wv.v[e]) - sg - xh * sgx);
+          if (dres) v += to_f(rv.v[e]);
+          o.v[e] = from_f<T>(v);
         }
         st16(dxr + vi * N, o);
       }
@@ -393,7 +509,7 @@ int pick_vpl(int H) {
 
 int norm_bwd_partials(int64_t rows) {
   int64_t blocks = (rows + kWaves - 1) / kWaves;
-  if (blocks > 256) blocks = 256;
+  if (blocks > kBwdBlocks) blocks = kBwdBlocks;
   if (blocks < 1) blocks = 1;
   return (int)blocks * kWaves;
 }
@@ -402,30 +518,49 @@ int norm_bwd_workspace_rows(int64_t rows) { return norm_bwd_partials(rows) + kSp
 
 int norm_max_hidden(int dtype) { return dtype == DT_F32 ? 32 * 64 * 4 : 32 * 64 * 8; }
 
-void rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H,
-                 float eps, int dt, hipStream_t s) {
+void rmsnorm_fwd(const void* x, const void* res, void* sum_out, const void* w, void* y,
+                 float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s) {
   const int64_t blocks = (rows + kWaves - 1) / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
     const int vpl = pick_vpl<T>(H);
     EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_fwd_k<T, V>), dim3(blocks), dim3(256), 0, s,
-                                           (const T*)x, (const T*)w, (T*)y, rstd, rows, H, eps));
+                                           (const T*)x, (const T*)res, (T*)sum_out, (const T*)w,
+                                           (T*)y, rstd, rows, H, eps));
   });
 }
 
-void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                 float* dw_part, void* dw, int64_t rows, int H, int dt, hipStream_t s) {
+template <typename T, int V, bool DW, bool FULL>
+void launch_rms_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                    const void* dres, void* dx, float* dw_part, int64_t rows, int H, int blocks,
+                    hipStream_t s) {
+  const size_t lds = (H * sizeof(T) + 15) / 16 * 16 + (DW ? kWaves * H * sizeof(float) : 0);
+  if (dres)
+    hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, DW, FULL, true>), dim3(blocks), dim3(256), lds, s,
+                       (const T*)dy, (const T*)x, (const T*)w, rstd, (const T*)dres, (T*)dx,
+                       dw_part, rows, H);
+  else
+    hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, DW, FULL, false>), dim3(blocks), dim3(256), lds, s,
+                       (const T*)dy, (const T*)x, (const T*)w, rstd, (const T*)dres, (T*)dx,
+                       dw_part, rows, H);
+}
+
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                 const void* dres, void* dx, float* dw_part, void* dw, int64_t rows, int H,
+                 int dt, hipStream_t s) {
   const int P = norm_bwd_partials(rows);
   const int blocks = P / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
     const int vpl = pick_vpl<T>(H);
-    if (vpl <= 8) {
-      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, true>), dim3(blocks),
-                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
-                                             (const T*)w, rstd, (T*)dx, dw_part, rows, H));
+    const bool full = H == vpl * 64 * (16 / (int)sizeof(T));
+    if (vpl <= 8 && H <= kLdsDwMaxH && full) {
+      EMA_VPL_SWITCH(vpl, (launch_rms_bwd<T, V, true, true>(dy, x, w, rstd, dres, dx, dw_part,
+                                                             rows, H, blocks, s)));
+    } else if (vpl <= 8 && H <= kLdsDwMaxH) {
+      EMA_VPL_SWITCH(vpl, (launch_rms_bwd<T, V, true, false>(dy, x, w, rstd, dres, dx, dw_part,
+                                                              rows, H, blocks, s)));
     } else {
-      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, false>), dim3(blocks),
-                                             dim3(256), 0, s, (const T*)dy, (const T*)x,
-                                             (const T*)w, rstd, (T*)dx, dw_part, rows, H));
+      EMA_VPL_SWITCH(vpl, (launch_rms_bwd<T, V, false, false>(dy, x, w, rstd, dres, dx, dw_part,
+                                                               rows, H, blocks, s)));
       const int64_t rpc = (rows + P - 1) / P;
       const int cblocks = (H / (16 / (int)sizeof(T)) + 255) / 256;
       hipLaunchKernelGGL((norm_dw_k<T, false>), dim3(cblocks, P), dim3(256), 0, s, (const T*)dy,
@@ -436,19 +571,21 @@ void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd
   });
 }
 
-void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
-                   float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s) {
+void layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                   void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
+                   hipStream_t s) {
   const int64_t blocks = (rows + kWaves - 1) / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
     const int vpl = pick_vpl<T>(H);
     EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_fwd_k<T, V>), dim3(blocks), dim3(256), 0, s,
-                                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean,
+                                           (const T*)x, (const T*)res, (T*)sum_out, (const T*)w,
+                                           (const T*)b, (T*)y, mean,
                                            rstd, rows, H, eps));
   });
 }
 
 void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
-                   const float* rstd, void* dx, float* dw_part, float* db_part, void* dw,
+                   const float* rstd, const void* dres, void* dx, float* dw_part, float* db_part, void* dw,
                    void* db, int64_t rows, int H, int dt, hipStream_t s) {
   const int P = norm_bwd_partials(rows);
   const int blocks = P / kWaves;
@@ -457,12 +594,14 @@ void layernorm_bwd(const void* dy, const void* x, const void* w, const float* me
     if (vpl <= 8) {
       EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_k<T, V, true>), dim3(blocks),
                                              dim3(256), 0, s, (const T*)dy, (const T*)x,
-                                             (const T*)w, mean, rstd, (T*)dx, dw_part, db_part,
+                                             (const T*)w, mean, rstd, (const T*)dres, (T*)dx,
+                                             dw_part, db_part,
                                              rows, H));
     } else {
       EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_k<T, V, false>), dim3(blocks),
                                              dim3(256), 0, s, (const T*)dy, (const T*)x,
-                                             (const T*)w, mean, rstd, (T*)dx, dw_part, db_part,
+                                             (const T*)w, mean, rstd, (const T*)dres, (T*)dx,
+                                             dw_part, db_part,
                                              rows, H));
       const int64_t rpc = (rows + P - 1) / P;
       const int cblocks = (H / (16 / (int)sizeof(T)) + 255) / 256;

@@ -357,8 +357,35 @@ class ParallelTransformerLayer(MegatronModule):
             out = make_viewless_tensor(out, requires_grad=out.requires_grad, keep_graph=True)
         return out
 
+    def _fused_residual_ok(self):
+        """Plain pre-LN block with nothing between the residual add and the
+        next norm (no dropout / drop-path / post-LN variants) -> the adds fold
+        into the norm kernels (``ops.norms.norm_residual``)."""
+        return (not self.use_post_ln and not self.parallel_attn and not self.parallel_layernorm
+                and not self.apply_residual_connection_post_layernorm
+                and not self.fp32_residual_connection and self.layer_type == LayerType.encoder
+                and (self.hidden_dropout == 0.0 or not self.training) and self.drop_path is None
+                and hasattr(self.input_layernorm, "forward_residual"))
+
+    def _forward_fused_residual(self, hidden_states, attention_mask, inference_params,
+                                position_ids):
+        ln_out, residual = self.input_layernorm.forward_residual(hidden_states)
+        attn_out, attn_bias = self.self_attention(ln_out, attention_mask,
+                                                  inference_params=inference_params,
+                                                  position_ids=position_ids)
+        if attn_bias is None:
+            ln_out, ln_in = self.post_attention_layernorm.forward_residual(attn_out, residual)
+        else:
+            ln_in = self._add(attn_out, attn_bias, residual)
+            ln_out = self.post_attention_layernorm(ln_in)
+        mlp_out, mlp_bias = self.mlp(ln_out)
+        return self._add(mlp_out, mlp_bias, ln_in, make_viewless=True)
+
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None,
                 inference_params=None, position_ids=None):
+        if self._fused_residual_ok():
+            return self._forward_fused_residual(hidden_states, attention_mask, inference_params,
+                                                position_ids)
         ln_out = self.input_layernorm(hidden_states)
         if self.fp32_residual_connection and ln_out.dtype == torch.float32:
             ln_out = ln_out.to(self.params_dtype)

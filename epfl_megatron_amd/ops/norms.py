@@ -27,14 +27,61 @@ def layer_norm_ref(x, weight, bias, eps):
                                           None if bias is None else bias.float(), eps).type_as(x)
 
 
+def _rows(t, h):
+    t2 = t.reshape(-1, h)
+    return t2 if t2.is_contiguous() else t2.contiguous()
+
+
+class _NormResidualFn(torch.autograd.Function):
+    """norm(s) and s, where s = x + res (res given) or s = x (pass-through).
+
+    Both outputs are returned so the block can use ``s`` as its residual
+    stream: in backward the residual gradient ``ds`` is added inside the norm
+    backward kernel (dx = norm'(dy) + ds), which replaces the two autograd
+    ``add`` kernels per block (fork of the residual, sum of its two grads).
+    """
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, eps, is_rms):
+        h = x.shape[-1]
+        x2 = _rows(x, h)
+        r2 = None if res is None else _rows(res, h)
+        if is_rms:
+            y, rstd, s = ext().rmsnorm_fwd(x2, weight, eps, r2)
+            ctx.save_for_backward(s, weight, rstd)
+        else:
+            y, mean, rstd, s = ext().layernorm_fwd(x2, weight, bias, eps, r2)
+            ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.is_rms = is_rms
+        ctx.has_res = res is not None
+        ctx.has_bias = bias is not None
+        ctx.shape = x.shape
+        s_out = s.view(x.shape) if res is not None else x
+        return y.view(x.shape), s_out
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        h = ctx.shape[-1]
+        dy2 = _rows(dy, h)
+        ds2 = None if ds is None else _rows(ds, h)
+        if ctx.is_rms:
+            s, weight, rstd = ctx.saved_tensors
+            dx, dw = ext().rmsnorm_bwd(dy2, s, weight, rstd, ds2)
+            db = None
+        else:
+            s, weight, mean, rstd = ctx.saved_tensors
+            dx, dw, db = ext().layernorm_bwd(dy2, s, weight, mean, rstd, ds2)
+            if not ctx.has_bias:
+                db = None
+        dx = dx.view(ctx.shape)
+        return dx, (dx if ctx.has_res else None), dw, db, None, None
+
+
 class _RMSNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, eps):
-        h = x.shape[-1]
-        x2 = x.reshape(-1, h)
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        y, rstd = ext().rmsnorm_fwd(x2, weight, eps)
+        x2 = _rows(x, x.shape[-1])
+        y, rstd, _ = ext().rmsnorm_fwd(x2, weight, eps)
         ctx.save_for_backward(x2, weight, rstd)
         ctx.shape = x.shape
         return y.view(x.shape)
@@ -42,21 +89,15 @@ class _RMSNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, weight, rstd = ctx.saved_tensors
-        dy2 = dy.reshape(-1, x2.shape[-1])
-        if not dy2.is_contiguous():
-            dy2 = dy2.contiguous()
-        dx, dw = ext().rmsnorm_bwd(dy2, x2, weight, rstd)
+        dx, dw = ext().rmsnorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, rstd)
         return dx.view(ctx.shape), dw, None
 
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps):
-        h = x.shape[-1]
-        x2 = x.reshape(-1, h)
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        y, mean, rstd = ext().layernorm_fwd(x2, weight, bias, eps)
+        x2 = _rows(x, x.shape[-1])
+        y, mean, rstd, _ = ext().layernorm_fwd(x2, weight, bias, eps)
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.has_bias = bias is not None
         ctx.shape = x.shape
@@ -65,10 +106,7 @@ class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, weight, mean, rstd = ctx.saved_tensors
-        dy2 = dy.reshape(-1, x2.shape[-1])
-        if not dy2.is_contiguous():
-            dy2 = dy2.contiguous()
-        dx, dw, db = ext().layernorm_bwd(dy2, x2, weight, mean, rstd)
+        dx, dw, db = ext().layernorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, mean, rstd)
         return dx.view(ctx.shape), dw, (db if ctx.has_bias else None), None
 
 
@@ -84,6 +122,15 @@ def layer_norm(x, weight, bias, eps):
     return layer_norm_ref(x, weight, bias, eps)
 
 
+def norm_residual(x, residual, weight, bias, eps, is_rms):
+    """(norm(x + residual), x + residual); residual=None -> (norm(x), x)."""
+    if use_native(x) and (residual is None or residual.dtype == x.dtype):
+        return _NormResidualFn.apply(x, residual, weight, bias, eps, is_rms)
+    s = x if residual is None else residual + x
+    y = rms_norm_ref(s, weight, eps) if is_rms else layer_norm_ref(s, weight, bias, eps)
+    return y, s
+
+
 class RMSNorm(torch.nn.Module):
     """Root-mean-square norm; ``weight`` init 1 (state-dict key ``weight``)."""
 
@@ -95,6 +142,9 @@ class RMSNorm(torch.nn.Module):
 
     def forward(self, x):
         return rms_norm(x, self.weight, self.eps)
+
+    def forward_residual(self, x, residual=None):
+        return norm_residual(x, residual, self.weight, None, self.eps, True)
 
 
 class MixedFusedLayerNorm(torch.nn.Module):
@@ -114,3 +164,6 @@ class MixedFusedLayerNorm(torch.nn.Module):
 
     def forward(self, x):
         return layer_norm(x, self.weight, self.bias, self.eps)
+
+    def forward_residual(self, x, residual=None):
+        return norm_residual(x, residual, self.weight, self.bias, self.eps, False)

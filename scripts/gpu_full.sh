@@ -9,6 +9,6 @@ tail -1 gpurun_out/bench_7b.log
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 2 --warmup 1 > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; }
   f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
-  python scripts/summarize_prof.py "$f" gpurun_out/prof_summary.csv "${PROF_TITLE:-rocprofv3 --kernel-trace --stats: Llama-2-7B bf16, 1x MI355X, seq 1024, mbs 8, 4 microbatches/step, bench.py --steps 2 --warmup 1}"
+  python scripts/summarize_prof.py "$f" gpurun_out/prof_summary.csv "${PROF_TITLE:-rocprofv3 --kernel-trace --stats: Llama-2-7B bf16, 1x MI355X, seq 1024, mbs 16, 2 microbatches/step, bench.py --steps 2 --warmup 1}"
   head -22 gpurun_out/prof_summary.csv | cut -c1-150
 fi

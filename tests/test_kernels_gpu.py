@@ -52,6 +52,43 @@ def test_rmsnorm(dtype, H):
     _close(w.grad, wr.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "rmsnorm dw")
 
 
+@pytest.mark.parametrize("is_rms", [True, False])
+@pytest.mark.parametrize("with_res", [True, False])
+@pytest.mark.parametrize("rows,H", [(37, 4096), (5003, 4096), (129, 12288)])
+def test_norm_residual_fused(is_rms, with_res, rows, H):
+    """norm_residual(x, res) == (norm(x + res), x + res), with the residual
+    gradient folded into the norm backward; rows > 2048 walks the software-
+    pipelined multi-row loop of the backward kernel (odd and even trips)."""
+    from epfl_megatron_amd.ops.norms import norm_residual
+    torch.manual_seed(2)
+    dt = torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    res = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(dt).requires_grad_()
+    b = None if is_rms else (0.1 * torch.randn(H, device=DEV)).to(dt).requires_grad_()
+    y, s = norm_residual(x, res, w, b, 1e-5, is_rms)
+    xr = x.detach().float().requires_grad_()
+    rr = res.detach().float().requires_grad_() if with_res else None
+    wr = w.detach().float().requires_grad_()
+    br = None if is_rms else b.detach().float().requires_grad_()
+    sr = xr + rr if with_res else xr
+    if is_rms:
+        yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = torch.nn.functional.layer_norm(sr, (H,), wr, br, 1e-5)
+    _close(s, sr, 2e-2, 1e-2, "residual sum")
+    _close(y, yr, 5e-2, 2e-2, "norm fwd")
+    g1, g2 = torch.randn_like(y), torch.randn_like(s)
+    ((y.float() * g1.float()).sum() + (s.float() * g2.float()).sum()).backward()
+    ((yr * g1.float()).sum() + (sr * g2.float()).sum()).backward()
+    _close(x.grad, xr.grad, 1e-1, 3e-2, "dx")
+    if with_res:
+        _close(res.grad, rr.grad, 1e-1, 3e-2, "dres")
+    _close(w.grad, wr.grad, 0.02 * rows ** 0.5, 3e-2, "dw")
+    if not is_rms:
+        _close(b.grad, br.grad, 0.02 * rows ** 0.5, 3e-2, "db")
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("H", [768, 8192])
 def test_layernorm(dtype, H):
