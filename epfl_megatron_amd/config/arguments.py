@@ -242,6 +242,8 @@ FLAG_TABLE = {
         _flag("--retriever_seq_length", type=int, default=256),
         _flag("--sample_rate", type=float, default=1.0),
         _flag("--mask_prob", type=float, default=0.15),
+        # upstream Megatron flag the reference's pretrain_bert.py reads but never defines
+        _flag("--bert_no_binary_head", action="store_false", dest="bert_binary_head"),
         _flag("--short_seq_prob", type=float, default=0.1),
         _flag("--mmap_warmup", action="store_true"),
         _flag("--num_workers", type=int, default=2),
@@ -444,6 +446,9 @@ def _derive_schedule_and_model(args):
         _require(args.encoder_num_layers is not None,
                  "either num_layers or encoder_num_layers should be specified")
         args.num_layers = args.encoder_num_layers
+    if args.decoder_num_layers is None:
+        # (the reference leaves it None and T5 then fails to build its decoder)
+        args.decoder_num_layers = args.num_layers
     for req in ("num_layers", "hidden_size", "num_attention_heads"):
         _require(getattr(args, req) is not None, f"{req} argument is None")
     if args.ffn_hidden_size is None:

@@ -4,13 +4,19 @@
 // so cached *_indexmap_*.npy files stay interchangeable:
 //   sample_index  : int32 [num_samples + 1, 2] = (position in doc_idx, token offset),
 //                   windows of seq_length + 1 tokens overlapping by one token;
-//   blend_indices : greedy "largest deficit" interleave of several datasets.
+//   blend_indices : greedy "largest deficit" interleave of several datasets;
+//   sentence_pair_mapping : BERT/T5 samples (first sentence, end sentence,
+//                   target length), shuffled with mt19937_64(seed + 1);
+//   block_mapping : ICT evidence blocks (first sentence, end sentence, doc, block id).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <iostream>
+#include <limits>
+#include <random>
 #include <stdexcept>
 #include <vector>
 
@@ -151,6 +157,143 @@ py::array_t<int64_t> stitch_samples(py::array tokens,
   return out;
 }
 
+// ---- sentence-level samples (BERT / T5 / ICT) ------------------------------
+// Reference: megatron/data/helpers.cpp build_mapping_impl :188-392 and
+// build_blocks_mapping_impl :454-656.  One pass that appends to a vector (the
+// reference counts in a first pass and fills in a second; with the same RNG
+// consumption the arrays are identical), then a Fisher-Yates shuffle driven
+// by mt19937_64(seed + 1) exactly as the reference so cached maps interchange.
+constexpr int32_t kLongSentence = 512;
+
+int32_t target_len(int32_t short_ratio, int32_t max_len, std::mt19937& gen) {
+  if (short_ratio == 0) return max_len;
+  const auto r = gen();
+  if (r % (uint64_t)short_ratio == 0) return (int32_t)(2 + r % (uint64_t)(max_len - 1));
+  return max_len;
+}
+
+bool has_long_sentence(const int32_t* sizes, int64_t first, int64_t last) {
+  for (int64_t i = first; i < last; ++i)
+    if (sizes[i] > kLongSentence) return true;
+  return false;
+}
+
+template <typename Idx>
+py::array shuffled(std::vector<uint64_t>& rows, int cols, int32_t seed) {
+  const int64_t n = (int64_t)rows.size() / cols;
+  std::mt19937_64 gen((uint64_t)(seed + 1));
+  for (int64_t i = n - 1; i > 0; --i) {
+    const int64_t j = (int64_t)(gen() % (uint64_t)(i + 1));
+    for (int c = 0; c < cols; ++c) std::swap(rows[i * cols + c], rows[j * cols + c]);
+  }
+  py::array_t<Idx> out({n, (int64_t)cols});
+  Idx* o = out.mutable_data();
+  for (int64_t k = 0; k < n * cols; ++k) o[k] = (Idx)rows[k];
+  return out;
+}
+
+py::array sentence_pair_mapping(py::array_t<int64_t, py::array::c_style | py::array::forcecast> docs,
+                                py::array_t<int32_t, py::array::c_style | py::array::forcecast> sizes,
+                                int32_t num_epochs, uint64_t max_num_samples,
+                                int32_t max_seq_length, double short_seq_prob, int32_t seed,
+                                bool verbose, int32_t min_num_sent) {
+  if (num_epochs <= 0 || max_seq_length <= 1 || short_seq_prob < 0.0 || short_seq_prob > 1.0 ||
+      seed <= 0)
+    throw std::invalid_argument("invalid mapping arguments");
+  const int64_t* d = docs.data();
+  const int32_t* sz = sizes.data();
+  const int64_t ndocs = docs.shape(0) - 1;
+  const int32_t short_ratio = short_seq_prob > 0 ? (int32_t)std::round(1.0 / short_seq_prob) : 0;
+  std::mt19937 gen((uint32_t)seed);
+  std::vector<uint64_t> rows;
+  uint64_t n = 0, empty = 0, one = 0, longd = 0;
+  for (int32_t epoch = 0; epoch < num_epochs && n < max_num_samples; ++epoch) {
+    for (int64_t doc = 0; doc < ndocs; ++doc) {
+      const int64_t first = d[doc], last = d[doc + 1];
+      int64_t remain = last - first;
+      if (epoch == 0) {
+        empty += remain == 0;
+        one += remain == 1;
+      }
+      const bool lng = remain > 1 && has_long_sentence(sz, first, last);
+      if (epoch == 0) longd += lng;
+      if (remain < min_num_sent || lng) continue;
+      int64_t start = first;
+      int32_t len = 0, nsent = 0;
+      int32_t target = target_len(short_ratio, max_seq_length, gen);
+      for (int64_t s = first; s < last; ++s) {
+        len += sz[s];
+        ++nsent;
+        --remain;
+        if ((len >= target && remain > 1 && nsent >= min_num_sent) || remain == 0) {
+          rows.push_back((uint64_t)start);
+          rows.push_back((uint64_t)(s + 1));
+          rows.push_back((uint64_t)target);
+          ++n;
+          start = s + 1;
+          target = target_len(short_ratio, max_seq_length, gen);
+          len = 0;
+          nsent = 0;
+        }
+      }
+    }
+  }
+  if (verbose)
+    std::cout << "    sentence-pair mapping: " << n << " samples (" << empty << " empty, " << one
+              << " one-sentence, " << longd << " long-sentence documents)" << std::endl;
+  if (sizes.size() > (py::ssize_t)std::numeric_limits<uint32_t>::max())
+    return shuffled<uint64_t>(rows, 3, seed);
+  return shuffled<uint32_t>(rows, 3, seed);
+}
+
+py::array block_mapping(py::array_t<int64_t, py::array::c_style | py::array::forcecast> docs,
+                        py::array_t<int32_t, py::array::c_style | py::array::forcecast> sizes,
+                        py::array_t<int32_t, py::array::c_style | py::array::forcecast> title_sizes,
+                        int32_t num_epochs, uint64_t max_num_samples, int32_t max_seq_length,
+                        int32_t seed, bool verbose, bool use_one_sent_blocks) {
+  if (num_epochs <= 0 || max_seq_length <= 1 || seed <= 0)
+    throw std::invalid_argument("invalid block mapping arguments");
+  const int64_t* d = docs.data();
+  const int32_t* sz = sizes.data();
+  const int32_t* tz = title_sizes.data();
+  const int64_t ndocs = docs.shape(0) - 1;
+  if (title_sizes.shape(0) < ndocs) throw std::invalid_argument("title sizes shorter than docs");
+  const int32_t min_sent = use_one_sent_blocks ? 1 : 2;
+  std::vector<uint64_t> rows;
+  uint64_t n = 0;
+  for (int32_t epoch = 0; epoch < num_epochs && n < max_num_samples; ++epoch) {
+    int64_t block_id = 0;
+    for (int64_t doc = 0; doc < ndocs; ++doc) {
+      const int64_t first = d[doc], last = d[doc + 1];
+      const int32_t target = max_seq_length - tz[doc];
+      int64_t remain = last - first;
+      if (remain < min_sent || has_long_sentence(sz, first, last)) continue;
+      int64_t start = first;
+      int32_t len = 0, nsent = 0;
+      for (int64_t s = first; s < last; ++s) {
+        len += sz[s];
+        ++nsent;
+        --remain;
+        if ((len >= target && remain >= min_sent && nsent >= min_sent) || remain == 0) {
+          rows.push_back((uint64_t)start);
+          rows.push_back((uint64_t)(s + 1));
+          rows.push_back((uint64_t)doc);
+          rows.push_back((uint64_t)block_id);
+          ++n;
+          ++block_id;
+          start = s + 1;
+          len = 0;
+          nsent = 0;
+        }
+      }
+    }
+  }
+  if (verbose) std::cout << "    block mapping: " << n << " blocks" << std::endl;
+  if (sizes.size() > (py::ssize_t)std::numeric_limits<uint32_t>::max())
+    return shuffled<uint64_t>(rows, 4, seed);
+  return shuffled<uint32_t>(rows, 4, seed);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_helpers, m) {
@@ -158,4 +301,6 @@ PYBIND11_MODULE(_helpers, m) {
   m.def("sample_index", &sample_index);
   m.def("blend_indices", &blend_indices);
   m.def("stitch_samples", &stitch_samples);
+  m.def("sentence_pair_mapping", &sentence_pair_mapping);
+  m.def("block_mapping", &block_mapping);
 }

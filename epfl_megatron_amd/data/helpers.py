@@ -30,3 +30,23 @@ def stitch_samples(tokens, pointers, sizes, doc_idx, sample_idx, samples, seq_le
                                    np.ascontiguousarray(sample_idx, dtype=np.int32),
                                    np.ascontiguousarray(np.atleast_1d(samples), dtype=np.int64),
                                    int(seq_length))
+
+
+def build_mapping(docs, sizes, num_epochs, max_num_samples, max_seq_length, short_seq_prob, seed,
+                  verbose, min_num_sent):
+    """BERT/T5 sentence samples ``[n, 3]`` = (first sentence, end sentence, target length)."""
+    return _helpers.sentence_pair_mapping(np.ascontiguousarray(docs, dtype=np.int64),
+                                          np.ascontiguousarray(sizes, dtype=np.int32),
+                                          int(num_epochs), int(max_num_samples),
+                                          int(max_seq_length), float(short_seq_prob), int(seed),
+                                          bool(verbose), int(min_num_sent))
+
+
+def build_blocks_mapping(docs, sizes, titles_sizes, num_epochs, max_num_samples, max_seq_length,
+                         seed, verbose, use_one_sent_blocks):
+    """ICT evidence blocks ``[n, 4]`` = (first sentence, end sentence, doc, block id)."""
+    return _helpers.block_mapping(np.ascontiguousarray(docs, dtype=np.int64),
+                                  np.ascontiguousarray(sizes, dtype=np.int32),
+                                  np.ascontiguousarray(titles_sizes, dtype=np.int32),
+                                  int(num_epochs), int(max_num_samples), int(max_seq_length),
+                                  int(seed), bool(verbose), bool(use_one_sent_blocks))

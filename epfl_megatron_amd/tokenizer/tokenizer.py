@@ -189,7 +189,9 @@ class BertWordPieceTokenizer(AbstractTokenizer):
 
     @property
     def inv_vocab(self):
-        return {i: t for t, i in self.tokenizer.get_vocab().items()}
+        # id order (HF's get_vocab() orders added tokens nondeterministically
+        # across processes; BERT/T5 masking draws random ids from this list)
+        return {i: t for t, i in sorted(self.tokenizer.get_vocab().items(), key=lambda kv: kv[1])}
 
     def tokenize(self, text):
         return self.tokenizer.convert_tokens_to_ids(self.tokenizer.tokenize(text))
