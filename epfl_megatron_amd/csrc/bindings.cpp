@@ -508,6 +508,28 @@ void wgrad_gemm_ablation(const at::Tensor& dy, const at::Tensor& x, at::Tensor g
                            cur_stream());
 }
 
+// ---------------------------------------------------------------- transpose
+bool transpose16_supported(int64_t rows, int64_t cols) {
+  return ema::transpose16_supported(rows, cols);
+}
+
+// dst[cols, rows] = src[rows, cols]^T (16-bit dtypes; rows, cols multiples of 64).
+void transpose16(const at::Tensor& src, at::Tensor dst) {
+  check_gpu(src, "src");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.is_contiguous() && dst.is_contiguous(),
+              "transpose16: contiguous 2-D tensors required");
+  TORCH_CHECK(src.element_size() == 2 && dst.scalar_type() == src.scalar_type(),
+              "transpose16: matching 16-bit dtypes required");
+  TORCH_CHECK(dst.device() == src.device(), "transpose16: tensors on different devices");
+  const int64_t R = src.size(0), C = src.size(1);
+  TORCH_CHECK(dst.size(0) == C && dst.size(1) == R, "transpose16: dst must be [cols, rows]");
+  TORCH_CHECK(ema::transpose16_supported(R, C),
+              "transpose16: rows and cols must be positive multiples of 64");
+  check_vec_aligned(src, "src");
+  check_vec_aligned(dst, "dst");
+  ema::transpose16(src.data_ptr(), dst.data_ptr(), R, C, cur_stream());
+}
+
 }  // namespace
 
 void register_gemm_lt(pybind11::module& m);
@@ -541,4 +563,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flat_adam", &flat_adam);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("transpose16", &transpose16);
+  m.def("transpose16_supported", &transpose16_supported);
 }

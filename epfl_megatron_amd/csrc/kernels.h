@@ -111,4 +111,9 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
                          int64_t K, int mode, hipStream_t s);
 bool flash_attn_supported(int hd, int dt);
 
+// ---- transpose.hip -------------------------------------------------------------------------------
+// dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.
+bool transpose16_supported(int64_t rows, int64_t cols);
+void transpose16(const void* src, void* dst, int64_t rows, int64_t cols, hipStream_t s);
+
 }  // namespace ema

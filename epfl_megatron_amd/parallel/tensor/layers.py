@@ -168,6 +168,53 @@ _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hipblaslt").lower() == "hip"
 # 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —
 # isolated timings with hot caches do not predict in-model kernel times.
 _TUNED_GEMM = os.environ.get("EMA_GEMM", "torch").lower() == "tuned"
+# Operand layouts: hipBLASLt runs "TN" problems (both operands contiguous
+# along the reduction dim) 15-20 % faster than the forms PyTorch issues for
+# dgrad / wgrad (profiles/r1_gemm_layouts_hipblaslt.json).  EMA_DGRAD_WT=1
+# (default) keeps a K-contiguous copy of every weight, rebuilt once per
+# training step by csrc/transpose.hip, so dX = dY (W^T)^T is a TN GEMM.
+# EMA_WGRAD_TN=1 also transposes dY and X so that
+# main_grad (+)= (dY^T) (X^T)^T is one.
+_DGRAD_WT = os.environ.get("EMA_DGRAD_WT", "1") != "0"
+_WGRAD_TN = os.environ.get("EMA_WGRAD_TN", "0") == "1"
+_WEIGHT_T_GEN = [0]  # 0: no training step in flight -> no cached transposes
+
+
+def new_weight_transpose_generation():
+    """Called by ``train_step``: parameters may have changed since the last step,
+    so every cached W^T is rebuilt on its first use in this step."""
+    _WEIGHT_T_GEN[0] += 1
+
+
+def _tn_ok(t):
+    return (t.is_cuda and t.dim() == 2 and t.dtype in (torch.bfloat16, torch.float16)
+            and t.is_contiguous() and t.data_ptr() % 16 == 0
+            and ext().transpose16_supported(t.shape[0], t.shape[1]))
+
+
+def _transpose(t):
+    out = torch.empty(t.shape[1], t.shape[0], dtype=t.dtype, device=t.device)
+    ext().transpose16(t, out)
+    return out
+
+
+def _weight_t(weight):
+    """Contiguous W^T built at most once per training step (None: not applicable)."""
+    gen = _WEIGHT_T_GEN[0]
+    if not (_DGRAD_WT and gen > 0 and _tn_ok(weight)):
+        return None
+    key = (gen, weight.data_ptr(), weight._version)
+    cached = getattr(weight, "_wt_cache", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    shape = (weight.shape[1], weight.shape[0])
+    if cached is not None and tuple(cached[1].shape) == shape and cached[1].dtype == weight.dtype:
+        wt = cached[1]
+    else:
+        wt = torch.empty(shape, dtype=weight.dtype, device=weight.device)
+    ext().transpose16(weight, wt)
+    weight._wt_cache = (key, wt)
+    return wt
 
 
 def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
@@ -190,6 +237,11 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
             ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
         elif _TUNED_GEMM:
             tuned_gemm.wgrad(main_grad.view(N, K), grad_output_2d, input_2d, accumulate)
+        elif _WGRAD_TN and _tn_ok(grad_output_2d) and _tn_ok(input_2d):
+            # token-contiguous operands: dY^T [N, M] and X^T [K, M] -> TN GEMM
+            torch.addmm(main_grad, _transpose(grad_output_2d), _transpose(input_2d).t(),
+                        beta=1.0 if accumulate else 0.0, out_dtype=torch.float32,
+                        out=main_grad)
         else:
             torch.addmm(main_grad, grad_output_2d.t(), input_2d, beta=1.0 if accumulate else 0.0,
                         out_dtype=torch.float32, out=main_grad)
@@ -243,7 +295,8 @@ class _LinearFn(torch.autograd.Function):
             grad_input = tuned_gemm.linear_dgrad(g2, weight).view(
                 *grad_output.shape[:-1], weight.shape[1])
         else:
-            grad_input = grad_output.matmul(weight)
+            wt = _weight_t(weight) if grad_output.is_cuda else None
+            grad_input = grad_output.matmul(weight) if wt is None else grad_output.matmul(wt.t())
         if gather_handle is not None:
             gather_handle.wait()
         go2 = grad_output.reshape(-1, grad_output.shape[-1])

@@ -25,6 +25,7 @@ from .parallel import state
 from .parallel.ddp import DistributedDataParallel as LocalDDP
 from .parallel.pipeline.schedules import get_forward_backward_func
 from .parallel.tensor import set_defaults_if_not_set_tensor_model_parallel_attributes
+from .parallel.tensor.layers import new_weight_transpose_generation
 from .utils.misc import (calc_params_l2_norm, check_adlr_autoresume_termination, print_all_nodes,
                          print_rank_0, print_rank_last, report_memory, unwrap_model)
 from .utils.flops import flops_per_token
@@ -225,6 +226,7 @@ def _setup_model_and_optimizer(model_provider_func, model_type, no_wd_decay_cond
 
 def train_step(forward_step_func, data_iterator, model, optimizer, opt_param_scheduler, args):
     timers = get_timers()
+    new_weight_transpose_generation()
     if args.DDP_impl == "local":
         for m in model:
             m.zero_grad_buffer()

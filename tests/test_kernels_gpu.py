@@ -402,6 +402,45 @@ def test_tuned_gemm_products(tmp_path, monkeypatch):
     _close(g, 2 * ref, atol=0.1, rtol=1e-3, msg="wgrad accumulate")
 
 
+@pytest.mark.parametrize("R,C", [(64, 64), (128, 320), (4096, 704)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_transpose16(R, C, dtype):
+    """csrc/transpose.hip: exact transpose (bit copy), shape gate."""
+    C_ = _ext()
+    torch.manual_seed(5)
+    x = torch.randn(R, C, device=DEV, dtype=dtype)
+    y = torch.full((C, R), float("nan"), device=DEV, dtype=dtype)
+    C_.transpose16(x, y)
+    assert torch.equal(y, x.t())
+    assert C_.transpose16_supported(R, C) and not C_.transpose16_supported(R + 32, C)
+
+
+@pytest.mark.parametrize("wgrad_tn", [False, True])
+def test_linear_tn_layouts(monkeypatch, wgrad_tn):
+    """dgrad through the cached W^T (and wgrad through transposed operands) equals the
+    plain products; a new training-step generation picks up an updated weight."""
+    from epfl_megatron_amd.parallel.tensor import layers as L
+    monkeypatch.setattr(L, "_WGRAD_TN", wgrad_tn)
+    monkeypatch.setattr(L, "_DGRAD_WT", True)
+    torch.manual_seed(4)
+    w = torch.nn.Parameter(torch.randn(384, 256, device=DEV, dtype=torch.bfloat16) * 0.05)
+    w.main_grad = torch.zeros(384, 256, device=DEV)
+    x = torch.randn(128, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    for step in range(2):
+        L.new_weight_transpose_generation()
+        w._mg_fresh = True
+        x.grad = None
+        y = L.linear_with_grad_accumulation_and_async_allreduce(x, w, None, True, False, False)
+        g = torch.randn_like(y)
+        y.backward(g)
+        assert w._wt_cache[1].shape == (256, 384)
+        _close(x.grad, g.float() @ w.detach().float(), atol=0.05, rtol=2e-2, msg=f"dgrad {step}")
+        _close(w.main_grad, g.float().t() @ x.detach().float(), atol=0.05, rtol=1e-2,
+               msg=f"wgrad {step}")
+        with torch.no_grad():
+            w.data.mul_(-0.5)  # an optimizer-style update that bypasses the version counter
+
+
 def test_flash_attention_bwd_kv_longer():
     """Backward with sk > sq (bottom-right causal alignment) and ragged tiles."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
