@@ -3,9 +3,10 @@
     python tasks/main.py --task {LAMBADA,WIKITEXT103} --valid_data FILE --load CKPT \
         --model_name llama2 ... [--overlapping_eval 32] [--strict_lambada]
 
-The GPT-family zero-shot tasks are implemented; the BERT-based finetuning
-tasks of the reference (RACE, MNLI, QQP, ICT / retriever) are legacy and
-are rejected with a clear error.
+Dispatch (reference tasks/main.py:82-94): RACE -> tasks.race, MNLI/QQP ->
+tasks.glue, LAMBADA/WIKITEXT103 -> tasks.zeroshot_gpt, ICT-ZEROSHOT-NQ /
+RETRIEVER-EVAL -> tasks.orqa.evaluate_orqa, RET-FINETUNE-NQ ->
+tasks.orqa.supervised.finetune.
 """
 import os
 import sys
@@ -49,10 +50,18 @@ def main(argv=None):
     if args.task in ("LAMBADA", "WIKITEXT103"):
         from tasks.zeroshot_gpt.evaluate import main as zeroshot
         return zeroshot()
-    if args.task in ("RACE", "MNLI", "QQP", "ICT-ZEROSHOT-NQ", "RETRIEVER-EVAL",
-                     "RET-FINETUNE-NQ"):
-        raise NotImplementedError(f"{args.task} is a BERT-family task (legacy in the "
-                                  "reference); only GPT-family zero-shot tasks are provided")
+    if args.task == "RACE":
+        from tasks.race.finetune import main as race
+        return race()
+    if args.task in ("MNLI", "QQP"):
+        from tasks.glue.finetune import main as glue
+        return glue()
+    if args.task in ("ICT-ZEROSHOT-NQ", "RETRIEVER-EVAL"):
+        from tasks.orqa.evaluate_orqa import main as orqa_eval
+        return orqa_eval()
+    if args.task == "RET-FINETUNE-NQ":
+        from tasks.orqa.supervised.finetune import main as ret_finetune
+        return ret_finetune()
     raise NotImplementedError(f"Task {args.task} is not implemented.")
 
 
