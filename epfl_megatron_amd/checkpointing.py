@@ -389,3 +389,33 @@ def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", stri
         dist.barrier()
     print_rank_0(f"  successfully loaded checkpoint from {load_dir} at iteration {iteration}")
     return iteration
+
+
+def load_biencoder_checkpoint(model, only_query_model=False, only_context_model=False,
+                              custom_load_path=None):
+    """Load just the retriever tower(s) needed for indexing / retrieval
+    (reference megatron/checkpointing.py:689-730; the reference reads an
+    undefined ``model_checkpoint_name`` there, here the resolved name is used
+    and ``release`` trackers are accepted)."""
+    from .utils.misc import unwrap_model
+    args = global_vars.get_args()
+    model = unwrap_model(model)
+    load_path = custom_load_path if custom_load_path is not None else args.load
+    iteration, release = _read_meta_local(get_checkpoint_tracker_filename(load_path))
+    name, _ = get_checkpoint_names(load_path, iteration, args.use_distributed_optimizer,
+                                   release=release)
+    if state.get_data_parallel_rank() == 0:
+        print(f"global rank {dist.get_rank() if dist.is_initialized() else 0} is loading "
+              f"checkpoint {name}", flush=True)
+    sd = dict(safe_load(name)["model"])
+    if only_query_model:
+        sd.pop("context_model", None)
+    if only_context_model:
+        sd.pop("query_model", None)
+    assert len(model) == 1
+    model[0].load_state_dict(sd)
+    if dist.is_initialized():
+        dist.barrier()
+    if state.get_data_parallel_rank() == 0:
+        print(f" successfully loaded {name}", flush=True)
+    return model
