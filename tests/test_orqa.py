@@ -166,3 +166,72 @@ def test_orqa_zeroshot_end_to_end(tmp_path, world):
         assert n_rows == 11
         assert got == pytest.approx(direct)
         assert 0 < direct[-1] and direct == sorted(direct)
+
+
+def _write_nq_json(path, n, seed):
+    import json
+    rng = np.random.default_rng(seed)
+
+    def ctx():
+        return {"title": f"w{int(rng.integers(0, 100))}",
+                "text": " ".join(f"w{int(x)}" for x in rng.integers(0, 100, 5))}
+    rows = [{"question": " ".join(f"w{int(x)}" for x in rng.integers(0, 100, 3)) + "?",
+             "answers": ["w1"], "positive_ctxs": [ctx()], "negative_ctxs": [ctx(), ctx()],
+             "hard_negative_ctxs": [ctx()]} for _ in range(n)]
+    with open(path, "w") as f:
+        json.dump(rows, f)
+    return str(path)
+
+
+def _ret_worker(rank, world, argv):
+    import tasks.main as tm
+    from epfl_megatron_amd.initialize import initialize_megatron
+    initialize_megatron(tm.get_tasks_args, {}, args_list=argv)
+    import tasks.finetune_utils as fu
+    import tasks.orqa.supervised.finetune as sf
+    seen = {"loss": [], "metrics": []}
+    orig_log = fu.training.training_log
+
+    def log(loss_dict, *a, **k):
+        if loss_dict:
+            seen["loss"].append(float(loss_dict["lm loss"]))
+        return orig_log(loss_dict, *a, **k)
+    fu.training.training_log = log
+    orig = sf.accuracy_func_provider
+
+    def provider(single):
+        f = orig(single)
+        return lambda model, epoch, output_predictions=False: seen["metrics"].append(
+            f(model, epoch))
+    sf.accuracy_func_provider = provider
+    sf.main()
+    return seen
+
+
+def test_supervised_retriever_finetune_dp_parity(tmp_path):
+    """DP=2 x mbs 2 gathers the same in-batch score matrix as DP=1 x mbs 4
+    (rows/columns permuted), so the losses agree step by step."""
+    from dist_utils import run_dist
+    vocab = tmp_path / "vocab.txt"
+    vocab.write_text("\n".join(WORDS) + "\n")
+    train = _write_nq_json(tmp_path / "train.json", 8, 0)
+    dev = _write_nq_json(tmp_path / "dev.json", 4, 1)
+    base = [a for a in BERT_TINY]
+    for flag in ("--train_iters",):
+        i = base.index(flag)
+        del base[i:i + 2]
+
+    def argv(mbs):
+        a = list(base)
+        a[a.index("--micro_batch_size") + 1] = str(mbs)
+        return a + ["--task", "RET-FINETUNE-NQ", "--vocab_file", str(vocab), "--train_data",
+                    train, "--valid_data", dev, "--epochs", "2", "--retriever_seq_length", "16",
+                    "--train_with_neg", "--train_hard_neg", "1", "--val_av_rank_hard_neg", "1",
+                    "--val_av_rank_other_neg", "1", "--retriever_report_topk_accuracies", "1",
+                    "3", "--eval_micro_batch_size", "2", "--keep_last"]
+    one = run_dist(_ret_worker, 1, argv(4))[0]
+    two = run_dist(_ret_worker, 2, argv(2))
+    assert len(one["loss"]) == 4 and all(np.isfinite(one["loss"]))
+    np.testing.assert_allclose(two[0]["loss"], one["loss"], rtol=2e-4)
+    for m in one["metrics"] + two[0]["metrics"]:
+        assert 0 <= m["rank"] and 0 <= m["top1_acc"] <= m["top3_acc"] <= 100
