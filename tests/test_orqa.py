@@ -235,3 +235,26 @@ def test_supervised_retriever_finetune_dp_parity(tmp_path):
     np.testing.assert_allclose(two[0]["loss"], one["loss"], rtol=2e-4)
     for m in one["metrics"] + two[0]["metrics"]:
         assert 0 <= m["rank"] and 0 <= m["top1_acc"] <= m["top3_acc"] <= 100
+
+
+@pytest.mark.gpu
+def test_mips_index_gpu_bf16():
+    """Device-resident bf16 index on the MI355X (MFMA GEMM + blocked top-k)
+    agrees with the fp32 CPU search up to bf16 ties."""
+    from epfl_megatron_amd.data.realm_index import MIPSIndex
+    rng = np.random.default_rng(1)
+    n, d = 200_000, 128
+    emb = rng.standard_normal((n, d)).astype(np.float16)
+    data = dict(zip(range(n), emb))
+    gpu = MIPSIndex(d, dict(data), use_gpu=True, block_rows=1 << 16)
+    assert gpu.embeds.is_cuda and gpu.embeds.dtype == torch.bfloat16
+    q = torch.from_numpy(rng.standard_normal((64, d)).astype(np.float32))
+    s_gpu, i_gpu = gpu.search_mips_index(q, 20, reconstruct=False)
+    full = q.numpy() @ emb.astype(np.float32).T
+    want = np.sort(full, axis=1)[:, ::-1][:, :20]
+    np.testing.assert_allclose(s_gpu, want, rtol=0.02, atol=0.3)
+    # the exact top-1 is found unless the runner-up is within bf16 rounding
+    top1 = np.argmax(full, axis=1)
+    gap = want[:, 0] - want[:, 1]
+    ok = (i_gpu[:, 0] == top1) | (gap < 0.2)
+    assert ok.all()
