@@ -4,7 +4,12 @@ Backed by the C++ module ``_helpers`` (built by ``epfl_megatron_amd.build``).
 """
 import numpy as np
 
-from . import _helpers
+try:
+    from . import _helpers
+except ImportError:  # fresh checkout: compile the (CPU-only, g++) module in-tree once
+    from ..build import build_data_helpers
+    build_data_helpers()
+    from . import _helpers
 
 
 def build_sample_idx(sizes, doc_idx, seq_length, num_epochs, tokens_per_epoch):
