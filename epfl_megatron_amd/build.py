@@ -99,7 +99,19 @@ def build_data_helpers(force=False):
     return out
 
 
+def build_dedup(force=False):
+    """``data/_dedup.so``: MinHash/LSH corpus de-duplication (CPU, g++)."""
+    import pybind11
+    src = os.path.join(CSRC, "dedup.cpp")
+    out = os.path.join(PKG, "data", "_dedup.so")
+    if force or _newer(out, [src]):
+        _run(["g++", "-O3", "-shared", "-std=c++17", "-fPIC", "-pthread", "-I",
+              pybind11.get_include(), "-I", sysconfig.get_paths()["include"], src, "-o", out])
+    return out
+
+
 def build_all(force=False, jobs=None):
+    build_dedup(force)
     h = build_data_helpers(force)
     k = build_kernels(force, jobs)
     return k, h
