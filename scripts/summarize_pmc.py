@@ -23,11 +23,17 @@ def main():
     out, dirs = sys.argv[1], sys.argv[2:]
     counters = defaultdict(lambda: defaultdict(float))
     time_ns, calls = defaultdict(float), defaultdict(int)
+    seen = set()  # a counter collected in several passes is taken from the first one
     for d in dirs:
+        here = set()
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
+                    if row["Counter_Name"] in seen:
+                        continue
+                    here.add(row["Counter_Name"])
                     counters[row["Kernel_Name"]][row["Counter_Name"]] += float(row["Counter_Value"])
+        seen |= here
         if d.endswith("_sq"):
             for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
                 with open(f) as fh:
