@@ -200,6 +200,9 @@ def wait_for_async_save():
 
 def save_checkpoint(iteration, model, optimizer, opt_param_scheduler):
     args = global_vars.get_args()
+    if optimizer is not None:
+        optimizer.resolve_pending()   # settle a lazily-checked skipped step
+        optimizer.wait_param_sync()   # dist-opt parameter all-gather in flight
     model = unwrap_model(model)
     wait_for_async_save()
     print_rank_0(f"saving checkpoint at iteration {iteration:7d} to {args.save}")

@@ -218,6 +218,9 @@ FLAG_TABLE = {
         _flag("--ddp_bucket_size_mb", type=float, default=256.0,
               help="fp32 gradient bucket size (MiB) for the overlapped DP reduction"),
         _flag("--no_overlap_grad_reduce", action="store_false", dest="overlap_grad_reduce"),
+        _flag("--no_overlap_param_gather", action="store_false", dest="overlap_param_gather",
+              help="dist-opt: all-gather parameters synchronously at step end instead of "
+                   "overlapping the gather with the next forward"),
         _flag("--allow_interleaved_pp2", action="store_true",
               help="lift the reference's PP>2 restriction for the interleaved schedule"),
         _flag("--distributed_timeout_minutes", type=int, default=10),
@@ -259,6 +262,9 @@ FLAG_TABLE = {
         # MI355X addition: synthetic data for benchmarks (no corpus needed).
         _flag("--synthetic_data", action="store_true"),
         _flag("--synthetic_vocab_size", type=int, default=32000),
+        _flag("--synthetic_pattern", type=str, default="uniform", choices=["uniform", "cycle"],
+              help="uniform: i.i.d. tokens; cycle: walk along a fixed random permutation "
+                   "(learnable, same cost)"),
     ],
     "autoresume": [
         _flag("--adlr_autoresume", action="store_true"),

@@ -371,7 +371,8 @@ at::Tensor chunked_sumsq(const at::Tensor& grad, const at::Tensor& table) {
 void flat_adam(at::Tensor master, const c10::optional<at::Tensor>& model_out, const at::Tensor& grad,
                at::Tensor m, at::Tensor v, const at::Tensor& table, std::vector<double> lrs,
                std::vector<double> wds, double beta1, double beta2, double eps, double bc1,
-               double bc2, double grad_scale, bool adam_w_mode) {
+               double bc2, double grad_scale, bool adam_w_mode,
+               const c10::optional<at::Tensor>& dev_state) {
   check_gpu(master, "master");
   check_table(table);
   for (const at::Tensor* t : {&master, &m, &v}) {
@@ -390,6 +391,13 @@ void flat_adam(at::Tensor master, const c10::optional<at::Tensor>& model_out, co
   a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
   a.bc1 = (float)bc1; a.bc2 = (float)bc2; a.grad_scale = (float)grad_scale;
   a.adam_w_mode = adam_w_mode ? 1 : 0;
+  a.dev_state = nullptr;
+  if (dev_state.has_value() && dev_state->defined()) {
+    check_gpu(*dev_state, "dev_state");
+    TORCH_CHECK(dev_state->scalar_type() == at::kFloat && dev_state->numel() >= 3 &&
+                dev_state->is_contiguous(), "dev_state must be fp32 [>=3]");
+    a.dev_state = dev_state->data_ptr<float>();
+  }
   void* mo = nullptr;
   int mdt = ema::DT_F32;
   if (model_out.has_value() && model_out->defined()) {
@@ -401,6 +409,23 @@ void flat_adam(at::Tensor master, const c10::optional<at::Tensor>& model_out, co
   }
   ema::flat_adam(master.data_ptr<float>(), mo, mdt, grad.data_ptr<float>(), m.data_ptr<float>(),
                  v.data_ptr<float>(), table.data_ptr<int64_t>(), (int)table.size(0), a, cur_stream());
+}
+
+void opt_prep(const at::Tensor& norm_sq, const c10::optional<at::Tensor>& inv_scale, double clip,
+              at::Tensor st) {
+  check_gpu(norm_sq, "norm_sq");
+  check_gpu(st, "st");
+  TORCH_CHECK(norm_sq.scalar_type() == at::kFloat && norm_sq.numel() == 1, "norm_sq: fp32 scalar");
+  TORCH_CHECK(st.scalar_type() == at::kFloat && st.numel() == 4 && st.is_contiguous(),
+              "st: fp32 [4]");
+  const float* inv = nullptr;
+  if (inv_scale.has_value() && inv_scale->defined()) {
+    check_gpu(*inv_scale, "inv_scale");
+    TORCH_CHECK(inv_scale->scalar_type() == at::kFloat && inv_scale->numel() == 1,
+                "inv_scale: fp32 scalar");
+    inv = inv_scale->data_ptr<float>();
+  }
+  ema::opt_prep(norm_sq.data_ptr<float>(), inv, (float)clip, st.data_ptr<float>(), cur_stream());
 }
 
 // ---------------------------------------------------------------- attention
@@ -561,6 +586,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_bwd", &softmax_bwd);
   m.def("chunked_sumsq", &chunked_sumsq);
   m.def("flat_adam", &flat_adam);
+  m.def("opt_prep", &opt_prep);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("transpose16", &transpose16);

@@ -16,6 +16,8 @@
 //
 // Query head j reads KV group j / (nq / nkv) directly (no K/V expansion).
 // Heavy causal blocks are launched first.  LSE is written in natural log.
+#include <cstdlib>
+
 #include "fa_common.h"
 #include "kernels.h"
 
@@ -234,6 +236,250 @@ void launch_fwd(const AttnParams& p, hipStream_t s) {
     hipLaunchKernelGGL((fa_fwd_k<T, HD, false>), grid, dim3(256), 0, s, p);
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: WAVES x 32 query rows per workgroup (WAVES = 8: 512 threads, a 256-row
+// query block, two waves per SIMD sharing every K/V tile), K/V double-buffered
+// in LDS with ONE barrier per tile: the next tile's global loads are issued
+// before this tile's MFMAs (T14) and written to the other LDS buffer after
+// them; the barrier at the end of the tile both publishes that buffer and
+// retires every read of the current one.  Query blocks are dispatched on a
+// flat grid, heaviest causal blocks of ALL heads first (the tail of a causal
+// launch is otherwise a few long blocks).
+template <typename T, int HD, bool CAUSAL, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnParams p) {
+  typedef typename MT<T>::x8 x8;
+  constexpr int NT = WAVES * 64;
+  constexpr int BMW = WAVES * 32;
+  constexpr int KS = HD / 16;
+  constexpr int DT = HD / 32;
+  constexpr int CPR = HD / 8;
+  constexpr int VST = HD + VPAD;
+  constexpr int KCH = (BN * CPR + NT - 1) / NT;  // chunks of K (and of V) per thread
+  constexpr int KTILE = BN * HD, VTILE = BN * VST;
+  __shared__ __attribute__((aligned(16))) T lds[2 * (KTILE + VTILE)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int nmb = (p.sq + BMW - 1) / BMW;
+  // flat grid: lin -> (query block, head, batch); heavy blocks first
+  const int nhb = p.nq * p.b;
+  const int lin = blockIdx.x;
+  const int mb = CAUSAL ? (nmb - 1 - lin / nhb) : lin / nhb;
+  const int hb = lin % nhb;
+  const int head = hb % p.nq, b = hb / p.nq;
+  const int r = p.nq / p.nkv, g = head / r;
+  const int off = p.sk - p.sq;
+
+  const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)(head % r) * p.q_sh;
+  const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
+  const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
+
+  const int m0 = mb * BMW + wave * 32;
+  const int qrow = m0 + c;
+  const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;
+
+  int n_end = p.sk;
+  if (CAUSAL) {
+    const int lim = mb * BMW + BMW + off;
+    n_end = lim < p.sk ? lim : p.sk;
+  }
+  const int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+  // this wave's own last useful tile (causal): later tiles are fully masked
+  int wtiles = ntiles;
+  if (CAUSAL) {
+    const int wl = m0 + 32 + off;
+    const int wt = wl > 0 ? (wl + BN - 1) / BN : 0;
+    wtiles = wt < ntiles ? wt : ntiles;
+  }
+
+  x8 kst[KCH], vst[KCH];
+  int krow[KCH];
+  bool kact[KCH];
+  int64_t koff[KCH], voff[KCH];
+#pragma unroll
+  for (int i = 0; i < KCH; ++i) {
+    const int idx = tid + NT * i;
+    kact[i] = idx < BN * CPR;
+    krow[i] = (idx / CPR) % BN;
+    koff[i] = (int64_t)krow[i] * p.k_ss + (idx % CPR) * 8;
+    voff[i] = (int64_t)krow[i] * p.v_ss + (idx % CPR) * 8;
+  }
+  auto load_tile = [&](int n0) {
+    const T* kt = K + (int64_t)n0 * p.k_ss;
+    const T* vt = V + (int64_t)n0 * p.v_ss;
+    if (n0 + BN <= p.sk) {
+#pragma unroll
+      for (int i = 0; i < KCH; ++i)
+        if (kact[i]) {
+          kst[i] = ld8(kt + koff[i]);
+          vst[i] = ld8(vt + voff[i]);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KCH; ++i)
+        if (kact[i]) {
+          const int64_t back = (n0 + krow[i] < p.sk) ? 0 : (int64_t)(n0 + krow[i] - (p.sk - 1));
+          kst[i] = ld8(kt + koff[i] - back * p.k_ss);
+          vst[i] = ld8(vt + voff[i] - back * p.v_ss);
+        }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    T* kl = lds + buf * (KTILE + VTILE);
+    T* vl = kl + KTILE;
+#pragma unroll
+    for (int i = 0; i < KCH; ++i)
+      if (kact[i]) {
+        const int idx = tid + NT * i;
+        const int row = idx / CPR, ch = idx % CPR;
+        *reinterpret_cast<x8*>(kl + sw_off<HD>(row, ch * 8)) = kst[i];
+        *reinterpret_cast<x8*>(vl + row * VST + ch * 8) = vst[i];
+      }
+  };
+
+  if (ntiles > 0) load_tile(0);
+  x8 qf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  if (ntiles > 0) store_tile(0);
+  __syncthreads();
+
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  for (int t = 0; t < ntiles; ++t) {
+    const int n0 = t * BN;
+    const int cur = t & 1;
+    if (t + 1 < ntiles) load_tile(n0 + BN);
+    const T* kl = lds + cur * (KTILE + VTILE);
+    const T* vl = kl + KTILE;
+
+    if (t < wtiles) {
+      f32x16 s0, s1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s0[i] = s1[i] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const x8 ka0 = *reinterpret_cast<const x8*>(kl + sw_off<HD>(c, kk * 16 + 8 * h));
+        const x8 ka1 = *reinterpret_cast<const x8*>(kl + sw_off<HD>(32 + c, kk * 16 + 8 * h));
+        s0 = MT<T>::mfma(ka0, qf[kk], s0);
+        s1 = MT<T>::mfma(ka1, qf[kk], s1);
+      }
+      const bool need_mask = CAUSAL ? (n0 + BN - 1 > m0 + off) : (n0 + BN > p.sk);
+      if (need_mask) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int k0 = n0 + acc_row(i, h), k1 = k0 + 32;
+          bool ok0 = k0 < p.sk, ok1 = k1 < p.sk;
+          if (CAUSAL) {
+            ok0 = ok0 && (k0 <= qrow + off);
+            ok1 = ok1 && (k1 <= qrow + off);
+          }
+          if (!ok0) s0[i] = -INFINITY;
+          if (!ok1) s1[i] = -INFINITY;
+        }
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2)
+        mt = fmaxf(mt, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      const float m_new = fmaxf(m_i, mt);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
+      float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sl2, -m_use));
+        s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sl2, -m_use));
+        rs0 += s0[i];
+        rs1 += s1[i];
+      }
+      float rs = rs0 + rs1;
+      rs += __shfl_xor(rs, 32, 64);
+      l_i = l_i * alpha + rs;
+      m_i = m_new;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      }
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const x8 pf = acc_frag<T>(sub == 0 ? s0 : s1, s);
+          const int kr = sub * 32 + 16 * s + 4 * h + tq;
+#pragma unroll
+          for (int d = 0; d < DT; ++d) {
+            const int col = d * 32 + (lane & 16) + 4 * tp;
+            const typename MT<T>::x4 va = MT<T>::tr_read(vl + kr * VST + col);
+            const typename MT<T>::x4 vb = MT<T>::tr_read(vl + (kr + 8) * VST + col);
+            o[d] = MT<T>::mfma(join<T>(va, vb), pf, o[d]);
+          }
+        }
+      }
+    }
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (qrow < p.sq) {
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    T* O = (T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow * p.o_ss + (int64_t)head * p.o_sh;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        typename MT<T>::x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (T)(o[d][4 * rg + e] * inv);
+        *reinterpret_cast<typename MT<T>::x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
+      }
+    }
+    if (h == 0) {
+      const float lse = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
+      p.lse[((int64_t)b * p.nq + head) * p.sq + qrow] = lse;
+    }
+  }
+}
+
+template <typename T, int HD, int WAVES>
+void launch_fwd2(const AttnParams& p, hipStream_t s) {
+  const int bmw = 32 * WAVES;
+  dim3 grid(((p.sq + bmw - 1) / bmw) * p.nq * p.b);
+  if (p.causal)
+    hipLaunchKernelGGL((fa_fwd2_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+  else
+    hipLaunchKernelGGL((fa_fwd2_k<T, HD, false, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+}
+
+// EMA_FA_FWD = 1 (round-1 kernel), 4 or 8 (waves per workgroup of fa_fwd2_k)
+int fwd_variant() {
+  static int v = [] {
+    const char* e = getenv("EMA_FA_FWD");
+    return e ? atoi(e) : 8;
+  }();
+  return v;
+}
+
+template <typename T, int HD>
+void launch_any(const AttnParams& p, hipStream_t s) {
+  const int v = fwd_variant();
+  if (v == 1) launch_fwd<T, HD>(p, s);
+  else if (v == 4) launch_fwd2<T, HD, 4>(p, s);
+  else launch_fwd2<T, HD, 8>(p, s);
+}
+
 }  // namespace
 }  // namespace fa
 
@@ -243,11 +489,11 @@ bool flash_attn_supported(int hd, int dt) {
 
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
   if (dt == DT_BF16) {
-    if (p.hd == 128) fa::launch_fwd<bf16, 128>(p, s);
-    else fa::launch_fwd<bf16, 64>(p, s);
+    if (p.hd == 128) fa::launch_any<bf16, 128>(p, s);
+    else fa::launch_any<bf16, 64>(p, s);
   } else {
-    if (p.hd == 128) fa::launch_fwd<fp16, 128>(p, s);
-    else fa::launch_fwd<fp16, 64>(p, s);
+    if (p.hd == 128) fa::launch_any<fp16, 128>(p, s);
+    else fa::launch_any<fp16, 64>(p, s);
   }
 }
 

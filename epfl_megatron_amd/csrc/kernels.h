@@ -69,7 +69,15 @@ struct AdamArgs {
   float wd[8];
   float beta1, beta2, eps, bc1, bc2, grad_scale;
   int adam_w_mode;
+  // Optional device step state written by opt_prep (nullptr: use the host
+  // scalars above): [0] grad scale (clip coef / loss scale), [1] skip flag
+  // (non-finite grad norm), [2] step count (bias correction).
+  const float* dev_state;
 };
+// One-thread epilogue of the grad-norm reduction: grad norm, clip coefficient,
+// non-finite flag and step count, all on the device (no host sync per step).
+// st = [scale, found_inf, step, grad_norm].
+void opt_prep(const float* norm_sq, const float* inv_scale, float clip, float* st, hipStream_t s);
 void flat_adam(float* master, void* model_out, int model_dt, const float* grad, float* m,
                float* v, const int64_t* table, int n_chunks, const AdamArgs& a, hipStream_t s);
 

@@ -58,14 +58,18 @@ __device__ __forceinline__ void store4(TO* p, float a, float b, float c, float d
   }
 }
 
+struct AdamScal {
+  float gs, bc1, bc2;
+};
+
 __device__ __forceinline__ float adam_elem(float& p, float g, float& m, float& v, float lr,
-                                           float wd, const AdamArgs& a) {
-  g *= a.grad_scale;
+                                           float wd, const AdamArgs& a, const AdamScal& c) {
+  g *= c.gs;
   if (!a.adam_w_mode) g += wd * p;
   m = a.beta1 * m + (1.f - a.beta1) * g;
   v = a.beta2 * v + (1.f - a.beta2) * g * g;
-  const float denom = sqrtf(v / a.bc2) + a.eps;
-  float upd = (m / a.bc1) / denom;
+  const float denom = sqrtf(v / c.bc2) + a.eps;
+  float upd = (m / c.bc1) / denom;
   if (a.adam_w_mode) upd += wd * p;
   p -= lr * upd;
   return p;
@@ -76,6 +80,14 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ master, TO* __
                                               const float* __restrict__ grad,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const int64_t* __restrict__ table, AdamArgs a) {
+  AdamScal c{a.grad_scale, a.bc1, a.bc2};
+  if (a.dev_state != nullptr) {
+    if (a.dev_state[1] != 0.f) return;  // non-finite grad norm: skip the step
+    const float step = a.dev_state[2];
+    c.gs = a.dev_state[0];
+    c.bc1 = 1.f - powf(a.beta1, step);
+    c.bc2 = 1.f - powf(a.beta2, step);
+  }
   const int64_t* row = table + 4 * (int64_t)blockIdx.x;
   const int64_t mo = row[0], bo = row[1], n = row[2];
   const int grp = (int)(row[3] & 0xFF);
@@ -90,10 +102,10 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ master, TO* __
     const float4 g = reinterpret_cast<const float4*>(G)[i];
     float4 mm = reinterpret_cast<float4*>(M)[i];
     float4 vv = reinterpret_cast<float4*>(Vv)[i];
-    adam_elem(p.x, g.x, mm.x, vv.x, lr, wd, a);
-    adam_elem(p.y, g.y, mm.y, vv.y, lr, wd, a);
-    adam_elem(p.z, g.z, mm.z, vv.z, lr, wd, a);
-    adam_elem(p.w, g.w, mm.w, vv.w, lr, wd, a);
+    adam_elem(p.x, g.x, mm.x, vv.x, lr, wd, a, c);
+    adam_elem(p.y, g.y, mm.y, vv.y, lr, wd, a, c);
+    adam_elem(p.z, g.z, mm.z, vv.z, lr, wd, a, c);
+    adam_elem(p.w, g.w, mm.w, vv.w, lr, wd, a, c);
     reinterpret_cast<float4*>(P)[i] = p;
     reinterpret_cast<float4*>(M)[i] = mm;
     reinterpret_cast<float4*>(Vv)[i] = vv;
@@ -101,7 +113,7 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ master, TO* __
   }
   for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
     float p = P[i], mm = M[i], vv = Vv[i];
-    adam_elem(p, G[i], mm, vv, lr, wd, a);
+    adam_elem(p, G[i], mm, vv, lr, wd, a, c);
     P[i] = p;
     M[i] = mm;
     Vv[i] = vv;
@@ -109,7 +121,29 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ master, TO* __
   }
 }
 
+__global__ void opt_prep_k(const float* __restrict__ norm_sq, const float* __restrict__ inv_scale,
+                           float clip, float* __restrict__ st) {
+  if (threadIdx.x != 0) return;
+  const float raw = norm_sq[0];
+  const bool bad = !isfinite(raw);
+  const float inv = inv_scale != nullptr ? inv_scale[0] : 1.f;
+  const float gn = sqrtf(raw) * inv;
+  float coef = 1.f;
+  if (clip > 0.f) {
+    const float cc = clip / (gn + 1.0e-6f);
+    if (cc < 1.f) coef = cc;
+  }
+  st[0] = bad ? 0.f : coef * inv;
+  st[1] = bad ? 1.f : 0.f;
+  st[2] = st[2] + (bad ? 0.f : 1.f);
+  st[3] = bad ? __builtin_nanf("") : gn;
+}
+
 }  // namespace
+
+void opt_prep(const float* norm_sq, const float* inv_scale, float clip, float* st, hipStream_t s) {
+  hipLaunchKernelGGL(opt_prep_k, dim3(1), dim3(64), 0, s, norm_sq, inv_scale, clip, st);
+}
 
 void chunked_sumsq(const float* grad, const int64_t* table, int n_chunks, float* partial,
                    float* out, hipStream_t s) {

@@ -31,6 +31,13 @@ class MegatronModule(torch.nn.Module):
         return self.state_dict(prefix=prefix, keep_vars=keep_vars)
 
     def word_embeddings_weight(self):
+        w = self._word_embeddings_weight()
+        wait = getattr(w, "_param_sync_wait", None)
+        if wait is not None:  # dist-opt: this param's all-gather may still be in flight
+            wait()
+        return w
+
+    def _word_embeddings_weight(self):
         lm = self.language_model
         if self.pre_process:
             return lm.embedding.word_embeddings.weight if lm.tie_embed_logits else lm.lm_head

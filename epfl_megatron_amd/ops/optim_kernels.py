@@ -61,21 +61,53 @@ def count_zeros(grad_buf, plan):
     return total
 
 
+def step_prep(norm_sq, inv_scale, clip, st):
+    """Device epilogue of the grad-norm reduction (no host sync):
+    ``st`` (fp32 [4]) <- [scale = clip_coef * inv_scale, found_inf, step (+1 unless
+    found_inf), grad_norm].  Reference semantics: ``optimizer.py:408-466`` (skip on
+    a non-finite norm, EPFL addition :442-444) and ``clip_grads.py:16-107``."""
+    if use_native(st):
+        ext().opt_prep(norm_sq.reshape(1).float(), inv_scale, float(clip), st)
+        return st
+    raw = norm_sq.reshape(()).float()
+    bad = ~torch.isfinite(raw)
+    inv = inv_scale.reshape(()).float() if inv_scale is not None else torch.ones_like(raw)
+    gn = torch.sqrt(raw) * inv
+    coef = torch.ones_like(raw)
+    if clip > 0.0:
+        coef = torch.clamp(clip / (gn + 1.0e-6), max=1.0)
+    st[0] = torch.where(bad, torch.zeros_like(raw), coef * inv)
+    st[1] = bad.float()
+    st[2] = st[2] + (~bad).float()
+    st[3] = torch.where(bad, torch.full_like(raw, float("nan")), gn)
+    return st
+
+
 def adam_step(master, model_out, grad_buf, exp_avg, exp_avg_sq, plan, lrs, wds, beta1, beta2,
-              eps, step, grad_scale, adam_w_mode=True):
+              eps, step, grad_scale, adam_w_mode=True, dev_state=None):
     """Fused AdamW over all chunks (apex FusedAdam math, bias correction on).
 
     ``grad_scale`` multiplies the gradient first (clip coef x 1/loss-scale).
     ``model_out`` (bf16/fp16 param buffer, same layout as ``grad_buf``) gets the
-    updated params in the same pass; None when master *is* the param buffer."""
-    bc1 = 1.0 - beta1 ** step
-    bc2 = 1.0 - beta2 ** step
+    updated params in the same pass; None when master *is* the param buffer.
+    ``dev_state`` (from ``step_prep``) replaces ``grad_scale`` / ``step`` with
+    device values and makes the update a no-op when the norm was non-finite."""
     if use_native(master):
+        bc1 = 1.0 - beta1 ** max(step, 1)
+        bc2 = 1.0 - beta2 ** max(step, 1)
         ext().flat_adam(master, model_out, grad_buf, exp_avg, exp_avg_sq, plan.table,
                         [float(x) for x in lrs], [float(x) for x in wds], float(beta1),
                         float(beta2), float(eps), float(bc1), float(bc2), float(grad_scale),
-                        bool(adam_w_mode))
+                        bool(adam_w_mode), dev_state)
         return
+    if dev_state is not None:
+        # CPU path: reading the device state is free (no GPU queue to drain)
+        if float(dev_state[1]) != 0.0:
+            return
+        grad_scale = float(dev_state[0])
+        step = int(round(float(dev_state[2])))
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
     for m_off, b_off, n, meta in plan.rows:
         if n == 0:
             continue
@@ -98,8 +130,15 @@ def adam_step(master, model_out, grad_buf, exp_avg, exp_avg_sq, plan, lrs, wds, 
             model_out[b_off:b_off + n].copy_(p)
 
 
-def sgd_step(master, model_out, grad_buf, momentum_buf, plan, lrs, wds, momentum, grad_scale):
-    """SGD with momentum (apex FusedSGD semantics: wd added to the grad)."""
+def sgd_step(master, model_out, grad_buf, momentum_buf, plan, lrs, wds, momentum, grad_scale,
+             dev_state=None):
+    """SGD with momentum (apex FusedSGD semantics: wd added to the grad).
+    With ``dev_state`` the scale is a device scalar and a skipped step is
+    masked on the device (no host sync)."""
+    skip = None
+    if dev_state is not None:
+        grad_scale = dev_state[0]
+        skip = dev_state[1] != 0
     for m_off, b_off, n, meta in plan.rows:
         if n == 0:
             continue
@@ -109,9 +148,15 @@ def sgd_step(master, model_out, grad_buf, momentum_buf, plan, lrs, wds, momentum
         g = grad_buf[b_off:b_off + n].float() * grad_scale + wd * p
         if momentum > 0:
             buf = momentum_buf[m_off:m_off + n]
-            buf.mul_(momentum).add_(g)
+            if skip is not None:
+                buf.copy_(torch.where(skip, buf, buf * momentum + g))
+            else:
+                buf.mul_(momentum).add_(g)
             g = buf
-        p.add_(g, alpha=-lr)
+        if skip is not None:
+            p.copy_(torch.where(skip, p, p - lr * g))
+        else:
+            p.add_(g, alpha=-lr)
         if model_out is not None:
             model_out[b_off:b_off + n].copy_(p)
 

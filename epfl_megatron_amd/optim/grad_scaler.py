@@ -1,4 +1,9 @@
-"""Loss scalers for fp16 (reference ``megatron/optimizer/grad_scaler.py``)."""
+"""Loss scalers for fp16 (reference ``megatron/optimizer/grad_scaler.py``).
+
+``update(found_inf)`` accepts a device bool/float tensor: the dynamic scaler
+keeps its growth / hysteresis trackers on the device and updates them with
+``torch.where`` so the optimizer step never waits for the GPU.  The checkpoint
+format (python ints for the trackers) is unchanged."""
 import torch
 
 
@@ -57,21 +62,30 @@ class DynamicGradScaler(MegatronGradScaler):
         self.backoff_factor = torch.tensor([backoff_factor], dtype=torch.float, device=dev)
         self.growth_interval = growth_interval
         self.hysteresis = hysteresis
-        self._growth_tracker = 0
-        self._hysteresis_tracker = hysteresis
+        self._growth = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._hyst = torch.full((1,), hysteresis, dtype=torch.int32, device=dev)
 
     def update(self, found_inf):
-        if found_inf:
-            self._growth_tracker = 0
-            self._hysteresis_tracker -= 1
-            if self._hysteresis_tracker <= 0:
-                self._scale = torch.max(self._scale * self.backoff_factor, self.min_scale)
-        else:
-            self._growth_tracker += 1
-            if self._growth_tracker == self.growth_interval:
-                self._growth_tracker = 0
-                self._hysteresis_tracker = self.hysteresis
-                self._scale = self._scale * self.growth_factor
+        dev = self._scale.device
+        found = torch.as_tensor(found_inf, device=dev).reshape(1).bool()
+        zero = torch.zeros_like(self._growth)
+        growth = torch.where(found, zero, self._growth + 1)
+        hyst = torch.where(found, self._hyst - 1, self._hyst)
+        backoff = found & (hyst <= 0)
+        scale = torch.where(backoff, torch.max(self._scale * self.backoff_factor, self.min_scale),
+                            self._scale)
+        grow = (~found) & (growth == self.growth_interval)
+        self._growth = torch.where(grow, zero, growth)
+        self._hyst = torch.where(grow, torch.full_like(hyst, self.hysteresis), hyst)
+        self._scale = torch.where(grow, scale * self.growth_factor, scale)
+
+    @property
+    def _growth_tracker(self):
+        return int(self._growth.item())
+
+    @property
+    def _hysteresis_tracker(self):
+        return int(self._hyst.item())
 
     def state_dict(self):
         return {"scale": self._scale, "growth_tracker": self._growth_tracker,
@@ -80,5 +94,5 @@ class DynamicGradScaler(MegatronGradScaler):
     def load_state_dict(self, sd):
         dev = self._scale.device
         self._scale = sd["scale"].to(dev)
-        self._growth_tracker = sd["growth_tracker"]
-        self._hysteresis_tracker = sd["hysteresis_tracker"]
+        self._growth.fill_(int(sd["growth_tracker"]))
+        self._hyst.fill_(int(sd["hysteresis_tracker"]))

@@ -73,6 +73,11 @@ class OptimizerParamScheduler:
             g["lr"] = lr * g.get("lr_mult", 1.0)
             g["weight_decay"] = wd * g.get("wd_mult", 1.0)
 
+    def rollback(self, increment):
+        """Undo ``step(increment)`` (the optimizer found the step skipped only
+        after the fact — its non-finite check runs on the device)."""
+        self.step(-increment)
+
     def state_dict(self):
         return {"max_lr": self.max_lr, "lr_warmup_steps": self.lr_warmup_steps,
                 "num_steps": self.num_steps, "lr_decay_style": self.lr_decay_style,

@@ -1,47 +1,197 @@
-"""Collective helpers.
+"""The one place collectives are issued from.
 
-On MI355X every collective here runs on RCCL (the ``nccl`` backend name in
-PyTorch-ROCm) over xGMI.  The CPU plumbing path (BASELINE config #1) runs the
-same code on ``gloo``, which lacks the fused tensor collectives; the helpers
-below pick the tensor form when the backend has it and an equivalent
-list-based form otherwise.  Nothing here changes *what* is communicated.
+Every tensor collective the framework runs (TP all-reduce / all-gather /
+reduce-scatter, DP bucket reduce-scatter / all-reduce, dist-opt parameter
+all-gather) goes through these helpers.  On MI355X they run on RCCL (the
+``nccl`` backend name in PyTorch-ROCm) over xGMI; on the CPU plumbing path they
+run the *same calls* on ``gloo`` (PyTorch >= 2.10 gloo implements
+``reduce_scatter_tensor``, ``all_gather_into_tensor`` and ``ReduceOp.AVG``,
+including the in-place forms), so the code the GPU runs is the code the CPU
+tests run — there is no backend fork.
+
+Two debug/observability aids live here:
+
+* **per-collective accounting** — every call adds (count, bytes) to a table
+  keyed by ``op/group-name``; with ``set_timing(True)`` (``--timing_log_level
+  2``) HIP events also measure launch->completion time per op.  ``training.py``
+  prints the table at each log interval (``report()``).
+* **in-flight race checker** — ``EMA_COMM_CHECK=1`` turns every async
+  collective into "snapshot at launch, verify + run at ``wait()``": if any
+  kernel or hook writes the buffer while the collective is logically in
+  flight, ``wait()`` raises.  RCCL gives no such guarantee checking, and a
+  write into a bucket that is being reduce-scattered silently corrupts
+  gradients; the CPU tests run with the checker on.
 """
+import os
+from collections import OrderedDict
+
 import torch
 import torch.distributed as dist
 
+_CHECK = os.environ.get("EMA_COMM_CHECK", "0") == "1"
+_TIMING = [False]
+_STATS = OrderedDict()  # key -> [count, bytes, ms]
+_GROUP_NAMES = {}
+_PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
 
-def _is_gloo(group):
-    try:
-        return dist.get_backend(group) == "gloo"
-    except Exception:  # pragma: no cover - uninitialized
-        return False
+
+class CommRaceError(RuntimeError):
+    pass
 
 
-def all_gather_into(output, inp, group, async_op=False):
-    """``output`` = concat over ranks of ``inp`` along dim 0."""
-    if _is_gloo(group):
-        world = dist.get_world_size(group)
-        chunks = list(output.chunk(world, dim=0))
-        tmp = [torch.empty_like(c) for c in chunks]
-        dist.all_gather(tmp, inp.contiguous(), group=group)
-        for c, t in zip(chunks, tmp):
-            c.copy_(t)
+def set_race_check(enabled):
+    global _CHECK
+    _CHECK = bool(enabled)
+
+
+def set_timing(enabled):
+    _TIMING[0] = bool(enabled)
+
+
+def name_group(group, name):
+    """Give a process group a readable name in the accounting table."""
+    _GROUP_NAMES[id(group)] = name
+
+
+def _key(op, group):
+    return f"{op}/{_GROUP_NAMES.get(id(group), 'world' if group is None else 'group')}"
+
+
+def _account(key, nbytes):
+    rec = _STATS.get(key)
+    if rec is None:
+        rec = _STATS[key] = [0, 0, 0.0]
+    rec[0] += 1
+    rec[1] += nbytes
+
+
+def _events_on(t):
+    return _TIMING[0] and t.is_cuda
+
+
+def _fold_events(block=False):
+    keep = []
+    for key, s, e in _PENDING_EVENTS:
+        if block or e.query():
+            _STATS[key][2] += s.elapsed_time(e)
+        else:
+            keep.append((key, s, e))
+    _PENDING_EVENTS[:] = keep
+
+
+def report(reset=True):
+    """{key: (count, bytes, ms)} since the last report."""
+    _fold_events(block=True)
+    out = {k: tuple(v) for k, v in _STATS.items()}
+    if reset:
+        _STATS.clear()
+    return out
+
+
+def format_report(rep):
+    parts = []
+    for k, (n, b, ms) in rep.items():
+        s = f"{k}: {n}x {b / 2**20:.1f} MiB"
+        if ms > 0:
+            s += f" {ms:.1f} ms ({b / 2**30 / max(ms, 1e-6) * 1e3:.1f} GiB/s)"
+        parts.append(s)
+    return " | ".join(parts)
+
+
+_INT_OF = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+
+
+def _bitwise_equal(a, b):
+    """Equality that treats NaN payloads as values (a NaN grad is not a race)."""
+    if a.is_floating_point():
+        it = _INT_OF[a.element_size()]
+        return torch.equal(a.contiguous().view(it), b.contiguous().view(it))
+    return torch.equal(a, b)
+
+
+class Work:
+    """Handle of an issued collective (``wait()`` makes the result visible to
+    the current stream)."""
+
+    __slots__ = ("_work", "_run", "_key", "_start", "_done", "_snap", "_watch")
+
+    def __init__(self, work=None, run=None, key=None, start=None, watch=None, snap=None):
+        self._work, self._run, self._key, self._start = work, run, key, start
+        self._watch, self._snap = watch, snap
+        self._done = False
+
+    def wait(self):
+        if self._done:
+            return
+        self._done = True
+        if self._run is not None:  # race-check mode: verify, then run for real
+            if not _bitwise_equal(self._watch, self._snap):
+                raise CommRaceError(
+                    f"{self._key}: buffer written while the collective was in flight "
+                    f"(between launch and wait)")
+            self._run()
+        elif self._work is not None:
+            self._work.wait()
+        if self._start is not None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            _PENDING_EVENTS.append((self._key, self._start, end))
+
+
+def _issue(op, group, tensor_for_bytes, watch, fn, async_op):
+    key = _key(op, group)
+    _account(key, tensor_for_bytes.numel() * tensor_for_bytes.element_size())
+    start = None
+    if _events_on(tensor_for_bytes):
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+    if async_op and _CHECK:
+        return Work(run=lambda: fn(False), key=key, start=start, watch=watch,
+                    snap=watch.detach().clone())
+    w = fn(async_op)
+    h = Work(work=w, key=key, start=start)
+    if not async_op:
+        h.wait()
         return None
-    return dist.all_gather_into_tensor(output, inp.contiguous(), group=group, async_op=async_op)
+    return h
 
 
-def reduce_scatter_into(output, inp, group, async_op=False, op=dist.ReduceOp.SUM):
-    """``output`` = this rank's dim-0 chunk of the sum over ranks of ``inp``."""
-    if _is_gloo(group):
-        world = dist.get_world_size(group)
-        rank = dist.get_rank(group)
-        tmp = inp.contiguous().clone()
-        dist.all_reduce(tmp, op=op, group=group)
-        output.copy_(tmp.chunk(world, dim=0)[rank])
-        return None
-    return dist.reduce_scatter_tensor(output, inp.contiguous(), op=op, group=group,
-                                      async_op=async_op)
+def _op(op):
+    if op == "avg":
+        return dist.ReduceOp.AVG
+    if op == "sum" or op is None:
+        return dist.ReduceOp.SUM
+    if op == "max":
+        return dist.ReduceOp.MAX
+    return op
 
 
-def all_reduce(tensor, group, async_op=False, op=dist.ReduceOp.SUM):
-    return dist.all_reduce(tensor, op=op, group=group, async_op=async_op)
+def all_reduce(tensor, group=None, async_op=False, op="sum"):
+    """In-place all-reduce; ``op='avg'`` averages inside the collective (ncclAvg)."""
+    rop = _op(op)
+    return _issue("all_reduce", group, tensor, tensor,
+                  lambda a: dist.all_reduce(tensor, op=rop, group=group, async_op=a), async_op)
+
+
+def reduce_scatter_into(output, inp, group=None, async_op=False, op="sum"):
+    """``output`` = this rank's dim-0 chunk of the reduction of ``inp`` over ranks.
+    ``output`` may alias the matching chunk of ``inp`` (in-place form)."""
+    rop = _op(op)
+    src = inp if inp.is_contiguous() else inp.contiguous()
+    return _issue("reduce_scatter", group, src, src,
+                  lambda a: dist.reduce_scatter_tensor(output, src, op=rop, group=group,
+                                                       async_op=a), async_op)
+
+
+def all_gather_into(output, inp, group=None, async_op=False):
+    """``output`` = concat over ranks of ``inp`` along dim 0.  ``inp`` may alias
+    this rank's chunk of ``output`` (in-place form)."""
+    src = inp if inp.is_contiguous() else inp.contiguous()
+    return _issue("all_gather", group, output, src,
+                  lambda a: dist.all_gather_into_tensor(output, src, group=group, async_op=a),
+                  async_op)
+
+
+def broadcast(tensor, src, group=None, async_op=False):
+    return _issue("broadcast", group, tensor, tensor,
+                  lambda a: dist.broadcast(tensor, src=src, group=group, async_op=a), async_op)

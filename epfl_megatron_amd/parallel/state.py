@@ -132,6 +132,12 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
                 _S.position_embedding_group = pg
             if rank in ranks:
                 _S.position_embedding_ranks = pos
+    from . import comm
+    for g, name in ((_S.dp_group, "dp"), (_S.mp_group, "mp"), (_S.tp_group, "tp"),
+                    (_S.pp_group, "pp"), (_S.embedding_group, "emb"),
+                    (_S.position_embedding_group, "posemb")):
+        if g is not None:
+            comm.name_group(g, name)
 
 
 def model_parallel_is_initialized():

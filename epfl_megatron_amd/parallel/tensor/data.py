@@ -2,6 +2,11 @@
 
 Only TP-rank 0 reads the dataset; it broadcasts sizes (one int64 vector)
 then one flat payload per dtype to the rest of its TP group.
+
+Host->device: the flat payload is staged in a small ring of pinned host
+buffers and copied with ``non_blocking=True``, so feeding a micro-batch never
+blocks the host on the GPU queue.  Without TP there is nothing to broadcast and
+the sizes come straight from the host tensors (no size round trip).
 """
 import torch
 import torch.distributed as dist
@@ -13,6 +18,39 @@ _MAX_DATA_DIM = 5
 
 def _device():
     return torch.cuda.current_device() if torch.cuda.is_available() else "cpu"
+
+
+class _PinnedRing:
+    """Reusable pinned staging buffers; a slot is reused only after the copy
+    that last read it has completed (event), which in steady state is long
+    before the ring wraps."""
+
+    def __init__(self, slots=4):
+        self.slots = [None] * slots
+        self.events = [None] * slots
+        self.i = 0
+
+    def to_device(self, cpu_flat, device):
+        if not torch.cuda.is_available() or device == "cpu":
+            return cpu_flat
+        k = self.i
+        self.i = (self.i + 1) % len(self.slots)
+        buf = self.slots[k]
+        n = cpu_flat.numel()
+        if buf is None or buf.numel() < n or buf.dtype != cpu_flat.dtype:
+            buf = torch.empty(max(n, 1), dtype=cpu_flat.dtype, pin_memory=True)
+            self.slots[k], self.events[k] = buf, None
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        buf[:n].copy_(cpu_flat)
+        out = buf[:n].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return out
+
+
+_RING = _PinnedRing()
 
 
 def _build_key_size_numel_dictionaries(keys, data):
@@ -45,14 +83,32 @@ def _build_key_size_numel_dictionaries(keys, data):
     return key_size, key_numel, total
 
 
+def _local_sizes(keys, data):
+    key_size, key_numel, total = {}, {}, 0
+    for key in keys:
+        shape = list(data[key].size())
+        if len(shape) >= _MAX_DATA_DIM:
+            raise AssertionError("you should increase MAX_DATA_DIM")
+        n = 1
+        for d in shape:
+            n *= d
+        key_size[key], key_numel[key] = shape, n
+        total += n
+    return key_size, key_numel, total
+
+
 def broadcast_data(keys, data, datatype):
-    key_size, key_numel, total = _build_key_size_numel_dictionaries(keys, data)
+    if state.get_tensor_model_parallel_world_size() == 1:
+        key_size, key_numel, total = _local_sizes(keys, data)
+    else:
+        key_size, key_numel, total = _build_key_size_numel_dictionaries(keys, data)
     if state.get_tensor_model_parallel_rank() == 0:
         for key in keys:
             if data[key].dtype != datatype:
                 raise AssertionError(f"{key} has data type {data[key].dtype} which is different "
                                      f"than {datatype}")
-        flat = torch.cat([data[k].contiguous().view(-1) for k in keys], dim=0).to(_device())
+        flat = torch.cat([data[k].contiguous().view(-1) for k in keys], dim=0)
+        flat = _RING.to_device(flat, _device()) if not flat.is_cuda else flat
     else:
         flat = torch.empty(total, device=_device(), dtype=datatype)
     if state.get_tensor_model_parallel_world_size() > 1:

@@ -21,6 +21,8 @@ from .checkpointing import load_checkpoint, save_checkpoint
 from .models.enums import ModelType
 from .models.module import Float16Module
 from .optim import get_megatron_optimizer, OptimizerParamScheduler
+from .optim.optimizer import LazyScalar
+from .parallel import comm
 from .parallel import state
 from .parallel.ddp import DistributedDataParallel as LocalDDP
 from .parallel.pipeline.schedules import get_forward_backward_func
@@ -166,7 +168,8 @@ def get_model(model_provider_func, model_type=ModelType.encoder_or_decoder, wrap
                               args.use_contiguous_buffers_in_local_ddp,
                               bucket_size_mb=args.ddp_bucket_size_mb,
                               overlap_grad_reduce=args.overlap_grad_reduce,
-                              use_distributed_optimizer=args.use_distributed_optimizer)
+                              use_distributed_optimizer=args.use_distributed_optimizer,
+                              overlap_param_gather=args.overlap_param_gather)
                      for m in model]
             if args.data_parallel_random_init:
                 for m in model:
@@ -242,12 +245,12 @@ def train_step(forward_step_func, data_iterator, model, optimizer, opt_param_sch
     timers("optimizer", log_level=1).start(barrier=args.barrier_with_L1_time)
     update_successful, grad_norm, num_zeros = optimizer.step(args, timers)
     timers("optimizer").stop()
-    if update_successful:
-        increment = get_num_microbatches() * args.micro_batch_size * args.data_parallel_size
-        opt_param_scheduler.step(increment=increment)
-        skipped_iter = 0
-    else:
-        skipped_iter = 1
+    # The skip decision is made on the device; the scheduler advances now and
+    # is rolled back by the optimizer if the step turns out to be skipped.
+    increment = get_num_microbatches() * args.micro_batch_size * args.data_parallel_size
+    opt_param_scheduler.step(increment=increment)
+    optimizer.register_scheduler_step(opt_param_scheduler, increment)
+    skipped_iter = LazyScalar(lambda: 0 if update_successful else 1)
     if args.empty_unused_memory_level >= 2 and torch.cuda.is_available():
         torch.cuda.empty_cache()
     if state.is_pipeline_last_stage(ignore_virtual=True):
@@ -260,10 +263,15 @@ def train_step(forward_step_func, data_iterator, model, optimizer, opt_param_sch
 
 
 def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scale,
-                 report_memory_flag, skipped_iter, grad_norm, params_norm, num_zeros_in_grad):
+                 skipped_iter, grad_norm, params_norm, num_zeros_in_grad, report_memory_flag):
     args = get_args()
     timers = get_timers()
     writer = get_tensorboard_writer()
+    # lazy device->host values of the step being logged (one iteration old)
+    skipped_iter = int(skipped_iter)
+    grad_norm = grad_norm.value() if isinstance(grad_norm, LazyScalar) else grad_norm
+    if callable(loss_scale):
+        loss_scale = loss_scale()
     adv, skp, nan = "advanced iterations", "skipped iterations", "nan iterations"
     if not skipped_iter:
         total_loss_dict[adv] = total_loss_dict.get(adv, 0) + 1
@@ -366,6 +374,10 @@ def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scal
             report_memory(f"(after {iteration} iterations)")
             report_memory_flag = False
         timers.log(timers_to_log, normalizer=args.log_interval)
+        if args.timing_log_level >= 1:
+            rep = comm.report()
+            if rep:
+                print_rank_last(" collectives (per interval): " + comm.format_report(rep))
     return report_memory_flag
 
 
@@ -386,9 +398,18 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
         m.train()
     total_loss_dict = {}
     iteration = args.iteration
+    comm.set_timing(args.timing_log_level >= 2)
     timers("interval-time", log_level=0).start(barrier=True)
     print_datetime("before the start of training step")
     report_memory_flag = True
+    pending_log = []
+
+    def flush_log():
+        nonlocal report_memory_flag
+        while pending_log:
+            report_memory_flag = training_log(*pending_log.pop(0),
+                                              report_memory_flag=report_memory_flag)
+
     while iteration < args.train_iters:
         update_num_microbatches(args.consumed_train_samples)
         args.curr_iteration = iteration
@@ -397,15 +418,26 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
         iteration += 1
         args.consumed_train_samples += state.get_data_parallel_world_size() * \
             args.micro_batch_size * get_num_microbatches()
-        loss_scale = float(optimizer.get_loss_scale().item()) if optimizer.grad_scaler else 1.0
-        params_norm = calc_params_l2_norm(model) if args.log_params_norm else None
-        report_memory_flag = training_log(loss_dict, total_loss_dict,
-                                          optimizer.param_groups[0]["lr"], iteration, loss_scale,
-                                          report_memory_flag, skipped_iter, grad_norm,
-                                          params_norm, num_zeros)
+        # Log the PREVIOUS iteration now that this one is enqueued: reading its
+        # loss / grad norm / skip flag then never stalls the GPU queue.
+        flush_log()
+        if optimizer.grad_scaler:
+            scale_t = optimizer.get_loss_scale().detach().clone()
+            loss_scale = (lambda t=scale_t: float(t.item()))
+        else:
+            loss_scale = 1.0
+        params_norm = None
+        if args.log_params_norm:
+            optimizer.wait_param_sync()
+            params_norm = calc_params_l2_norm(model)
+        pending_log.append((loss_dict, total_loss_dict, optimizer.param_groups[0]["lr"],
+                            iteration, loss_scale, skipped_iter, grad_norm, params_norm,
+                            num_zeros))
         if args.adlr_autoresume and iteration % args.adlr_autoresume_interval == 0:
+            flush_log()
             check_adlr_autoresume_termination(iteration, model, optimizer, opt_param_scheduler)
         if args.eval_interval and iteration % args.eval_interval == 0 and args.do_valid:
+            flush_log()
             evaluate_and_print_results(f"iteration {iteration}", forward_step_func,
                                        valid_data_iterator, model, iteration,
                                        process_non_loss_data_func, verbose=False, args=args)
@@ -415,10 +447,12 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
         saved = False
         if args.exit_signal_handler:
             if any(get_signal_handler().signals_received()):
+                flush_log()
                 save_checkpoint_and_time(iteration, model, optimizer, opt_param_scheduler)
                 print_datetime("exiting program after receiving SIGTERM.")
                 sys.exit()
         if args.save and args.save_interval and iteration % args.save_interval == 0:
+            flush_log()
             save_checkpoint_and_time(iteration, model, optimizer, opt_param_scheduler)
             saved = True
         if args.exit_duration_in_mins:
@@ -427,16 +461,21 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
                                 device=_device() if args.distributed_backend != "gloo" else "cpu")
             dist.all_reduce(done, op=dist.ReduceOp.MAX)
             if done.item():
+                flush_log()
                 if not saved:
                     save_checkpoint_and_time(iteration, model, optimizer, opt_param_scheduler)
                 print_datetime(f"exiting program after {train_time} minutes")
                 sys.exit()
         if args.exit_interval and iteration % args.exit_interval == 0:
+            flush_log()
             if not saved:
                 save_checkpoint_and_time(iteration, model, optimizer, opt_param_scheduler)
             dist.barrier()
             print_datetime(f"exiting program at iteration {iteration}")
             sys.exit()
+    flush_log()
+    optimizer.resolve_pending()
+    optimizer.wait_param_sync()
     return iteration
 
 

@@ -25,4 +25,8 @@ def non_embedding_params(args):
 
 def flops_per_token(args, seq_length=None):
     s = seq_length or args.seq_length
-    return 6.0 * non_embedding_params(args) + 12.0 * args.num_layers * args.hidden_size * s
+    # attention score/context GEMMs: 12 * L * (nq * hd) * s  (= 12 L h s unless
+    # --kv_channels decouples the projection width from h, e.g. the TP proxies)
+    hd = args.kv_channels or args.hidden_size // args.num_attention_heads
+    proj = hd * args.num_attention_heads
+    return 6.0 * non_embedding_params(args) + 12.0 * args.num_layers * proj * s

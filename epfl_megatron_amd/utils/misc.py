@@ -29,6 +29,8 @@ def calc_params_l2_norm(model):
     models = model if isinstance(model, list) else [model]
     sq = None
     for m in models:
+        if hasattr(m, "wait_param_sync"):  # dist-opt all-gather may be in flight
+            m.wait_param_sync()
         for p in m.parameters():
             if param_is_not_shared(p) and param_is_not_tensor_parallel_duplicate(p):
                 v = p.detach().float().pow(2).sum()
@@ -42,10 +44,11 @@ def calc_params_l2_norm(model):
 
 
 def average_losses_across_data_parallel_group(losses):
+    """Logging-only DP average (one fused collective, averaged inside it)."""
     averaged = torch.cat([l.clone().detach().view(1) for l in losses])
-    if dist.is_initialized():
-        dist.all_reduce(averaged, group=state.get_data_parallel_group())
-        averaged = averaged / dist.get_world_size(group=state.get_data_parallel_group())
+    if dist.is_initialized() and state.get_data_parallel_world_size() > 1:
+        from ..parallel import comm
+        comm.all_reduce(averaged, group=state.get_data_parallel_group(), op="avg")
     return averaged
 
 

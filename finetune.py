@@ -85,7 +85,8 @@ def train_valid_test_datasets_provider(train_val_test_num_samples):
         print_rank_0("> building synthetic train, validation, and test datasets ...")
         vocab = get_tokenizer().vocab_size
         return synthetic_train_valid_test_datasets(train_val_test_num_samples, args.seq_length,
-                                                   vocab, args.seed)
+                                                   vocab, args.seed,
+                                                   pattern=args.synthetic_pattern)
     from epfl_megatron_amd.data.gpt_dataset import build_train_valid_test_datasets
     print_rank_0("> building train, validation, and test datasets for GPT ...")
     train_ds, valid_ds, test_ds = build_train_valid_test_datasets(

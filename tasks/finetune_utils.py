@@ -128,8 +128,8 @@ def _train(model, optimizer, opt_param_scheduler, forward_step, train_dataloader
                 params_norm = calc_params_l2_norm(model)
             report_memory_flag = training.training_log(
                 losses, losses_dict_sum, optimizer.param_groups[0]["lr"], iteration,
-                float(optimizer.get_loss_scale()), report_memory_flag, skipped, grad_norm,
-                params_norm, nz)
+                float(optimizer.get_loss_scale()), skipped, grad_norm, params_norm, nz,
+                report_memory_flag=report_memory_flag)
             saved = False
             if args.save and args.save_interval and iteration % args.save_interval == 0:
                 save_checkpoint(iteration, model, optimizer, opt_param_scheduler)

@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# Every async collective in the tests runs under the in-flight race checker
+# (parallel/comm.py): a write into a buffer between launch and wait() fails.
+os.environ.setdefault("EMA_COMM_CHECK", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

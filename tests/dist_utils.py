@@ -20,10 +20,12 @@ def free_port():
     return p
 
 
-def _worker(rank, world, port, fn, args, q):
+def _worker(rank, world, port, fn, args, q, env=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+    if env:
+        os.environ.update(env)
     import torch
     torch.set_num_threads(1)
     try:
@@ -41,11 +43,13 @@ def _worker(rank, world, port, fn, args, q):
                 pass
 
 
-def run_dist(fn, world_size, *args, timeout=600):
+def run_dist(fn, world_size, *args, timeout=600, env=None):
+    """``env``: extra environment for the ranks, applied before the GPU is
+    touched (e.g. ``HIP_VISIBLE_DEVICES=""`` for a CPU reference run)."""
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, q))
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, q, env))
              for r in range(world_size)]
     for p in procs:
         p.start()

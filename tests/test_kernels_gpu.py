@@ -295,6 +295,35 @@ def test_flash_attention_odd_lengths(s):
     _attn_case(1, s, 4, 2, 128, torch.bfloat16, True, seed=s)
 
 
+def test_flash_attention_seq4096():
+    """The Llama-2 native context (BASELINE config #3 shape per head)."""
+    _attn_case(1, 4096, 4, 4, 128, torch.bfloat16, True, seed=41)
+
+
+@pytest.mark.parametrize("nq,nkv", [(71, 1), (32, 2), (16, 8)])
+def test_flash_attention_falcon_shapes(nq, nkv):
+    """Falcon head layouts at head_dim 64: 7B MQA (71/1), 40B-TP4-like (32/2), GQA (16/8)."""
+    _attn_case(1, 320, nq, nkv, 64, torch.bfloat16, True, seed=nq)
+
+
+def test_flash_attention_running_max_jump():
+    """Online-softmax rescale branch forced: one key row aligned with one query
+    row so that row's running max jumps by a large margin at a late tile
+    (rule: a rare data-dependent branch needs its own test)."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    torch.manual_seed(77)
+    b, s, nq, hd = 1, 640, 2, 128
+    q = torch.randn(b, s, nq, hd, device=DEV)
+    k = torch.randn(b, s, nq, hd, device=DEV) * 0.3
+    v = torch.randn(b, s, nq, hd, device=DEV)
+    for row, key in ((600, 530), (301, 300), (64, 5)):
+        k[:, key] = q[:, row] * 2.0  # score(row, key) >> every other score of the row
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    o = flash_attn_func(q, k, v, causal=True)
+    orf = attention_ref(q.float(), k.float(), v.float(), causal=True)
+    _close(o, orf, 2e-2, 2e-2, "flash fwd with running-max jumps")
+
+
 def test_flash_attention_fp16():
     _attn_case(1, 192, 4, 4, 128, torch.float16, True)
 

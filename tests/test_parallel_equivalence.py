@@ -80,6 +80,7 @@ def _train(rank, world, argv, steps):
     losses = []
     for _ in range(steps):
         ld, skipped, gnorm, _ = train_step(finetune.forward_step, train_it, model, opt, sched, args)
+        gnorm = None if gnorm is None else float(gnorm)
         args.consumed_train_samples += args.global_batch_size
         if ld:
             losses.append((float(ld["lm loss"]), gnorm))
@@ -180,3 +181,120 @@ def test_gpt_parallel(gpt_ref, extra):
     got = _losses(run_dist(_train, 2, TINY_GPT + extra + ["--micro_batch_size", "2",
                                                            "--global_batch_size", "4"], 3))
     _check(gpt_ref, got)
+
+
+# --------------------------------------------------------------------------
+# Round-2 coverage: the BASELINE shapes in miniature, tied embeddings with
+# DP > 1 (contribution counting), dist-opt with PP (embedding all-reduce
+# before the reduce-scatter), SP with DP > 1 (no write into a bucket in
+# flight: the race checker of parallel/comm.py is on for every test).
+
+def _mb(m, g):
+    return ["--micro_batch_size", str(m), "--global_batch_size", str(g)]
+
+
+def _set(argv, flag, value):
+    argv = list(argv)
+    if flag in argv:
+        argv[argv.index(flag) + 1] = value
+    else:
+        argv += [flag, value]
+    return argv
+
+
+@pytest.mark.parametrize("extra", [
+    [],
+    ["--use_distributed_optimizer"],
+])
+def test_gpt_tied_embeddings_data_parallel(extra):
+    base = _losses(run_dist(_train, 1, TINY_GPT + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 2, TINY_GPT + _mb(1, 4) + extra, 3))
+    _check(base, got)
+
+
+def test_gpt_pp_dp_distributed_optimizer():
+    """Tied embeddings across PP stages + dist-opt: the embedding-group sum must
+    precede the DP reduce-scatter."""
+    base = _losses(run_dist(_train, 1, TINY_GPT + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 4, TINY_GPT + _mb(1, 4) + [
+        "--pipeline_model_parallel_size", "2", "--use_distributed_optimizer"], 3))
+    _check(base, got)
+
+
+def test_llama_sp_dp_distributed_optimizer():
+    """SP norm-grad TP sums after the async DP reduce-scatter has completed."""
+    base = _losses(run_dist(_train, 1, TINY_LLAMA + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 4, TINY_LLAMA + _mb(1, 4) + [
+        "--tensor_model_parallel_size", "2", "--sequence_parallel",
+        "--use_distributed_optimizer"], 3))
+    _check(base, got, tol=5e-5)
+
+
+TINY_GQA = _set(_set(TINY_LLAMA, "--num_attention_heads", "8"), "--ffn_hidden_size", "128") + \
+    ["--num_attention_heads_kv", "2"]
+
+
+@pytest.mark.parametrize("tp", [2])
+def test_llama_gqa_tensor_parallel_one_group_per_rank(tp):
+    """70B-style GQA at TP = nkv: exactly one KV group per rank."""
+    base = _losses(run_dist(_train, 1, TINY_GQA + _mb(2, 4), 3))
+    got = _losses(run_dist(_train, tp, TINY_GQA + _mb(2, 4) + [
+        "--tensor_model_parallel_size", str(tp), "--sequence_parallel"], 3))
+    _check(base, got, tol=5e-5)
+
+
+TINY_LLAMA8 = _set(TINY_LLAMA, "--num_attention_heads", "8")
+
+
+@pytest.mark.parametrize("tp", [4, 8])
+def test_llama_wide_tensor_parallel(tp):
+    base = _losses(run_dist(_train, 1, TINY_LLAMA8 + _mb(2, 2), 2))
+    got = _losses(run_dist(_train, tp, TINY_LLAMA8 + _mb(2, 2) + [
+        "--tensor_model_parallel_size", str(tp), "--sequence_parallel"], 2))
+    _check(base, got, tol=5e-5)
+
+
+TINY_FALCON = ["--num_layers", "4", "--hidden_size", "64", "--num_attention_heads", "8",
+               "--num_attention_heads_kv", "2", "--seq_length", "16",
+               "--max_position_embeddings", "32", "--position_embedding_type", "rotary",
+               "--parallel_attn", "--parallel_layernorm", "--hidden_dropout", "0.0",
+               "--attention_dropout", "0.0", "--no_bias_gelu_fusion", "--no_bias_dropout_fusion",
+               "--tokenizer_type", "NullTokenizer", "--synthetic_vocab_size", "250",
+               "--make_vocab_size_divisible_by", "8", "--use_cpu_initialization",
+               "--model_name", "falcon", "--lr", "1e-3", "--train_iters", "4", "--seed", "1234",
+               "--log_interval", "1000", "--eval_iters", "0", "--eval_interval", "1000",
+               "--synthetic_data", "--clip_grad", "1.0"]
+
+
+def test_falcon_tp_pp_interleaved():
+    """BASELINE config #4 in miniature: Falcon (parallel attn + parallel LN, GQA,
+    tied embeddings) at TP=2 x PP=2 with the interleaved schedule."""
+    base = _losses(run_dist(_train, 1, TINY_FALCON + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 4, TINY_FALCON + _mb(1, 4) + [
+        "--tensor_model_parallel_size", "2", "--pipeline_model_parallel_size", "2",
+        "--num_layers_per_virtual_pipeline_stage", "1", "--allow_interleaved_pp2",
+        "--sequence_parallel"], 3))
+    _check(base, got, tol=5e-5)
+
+
+def test_falcon_data_parallel_distributed_optimizer():
+    base = _losses(run_dist(_train, 1, TINY_FALCON + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 2, TINY_FALCON + _mb(1, 4) +
+                           ["--use_distributed_optimizer"], 3))
+    _check(base, got)
+
+
+def test_llama_full_recompute_sp_distributed_activations():
+    base = _losses(run_dist(_train, 1, TINY_LLAMA + _mb(2, 4), 3))
+    got = _losses(run_dist(_train, 2, TINY_LLAMA + _mb(2, 4) + [
+        "--tensor_model_parallel_size", "2", "--sequence_parallel",
+        "--recompute_granularity", "full", "--recompute_method", "uniform",
+        "--recompute_num_layers", "1", "--distribute_saved_activations"], 3))
+    _check(base, got, tol=5e-5)
+
+
+def test_llama_pp_distributed_optimizer():
+    base = _losses(run_dist(_train, 1, TINY_LLAMA + _mb(1, 4), 3))
+    got = _losses(run_dist(_train, 4, TINY_LLAMA + _mb(1, 4) + [
+        "--pipeline_model_parallel_size", "2", "--use_distributed_optimizer"], 3))
+    _check(base, got)
