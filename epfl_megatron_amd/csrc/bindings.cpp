@@ -500,8 +500,10 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   p.dq = dq.data_ptr();
   p.dk = dk.data_ptr();
   p.dv = dv.data_ptr();
-  auto delta = at::empty({b * nq * sq}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({3 * b * nq * sq}, q.options().dtype(at::kFloat));
   p.delta = delta.data_ptr<float>();
+  p.ndelta = p.delta + b * nq * sq;
+  p.lse2 = p.ndelta + b * nq * sq;
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 

@@ -6,6 +6,8 @@
 // An accumulator used as the next MFMA's B operand: registers 8s..8s+7 form
 // k-step s with k = 16s + 8(j>>2) + 4h + (j&3) (j = element, h = lane>>5).
 #pragma once
+#include <utility>
+
 #include "common.h"
 
 namespace ema {
@@ -109,6 +111,40 @@ __device__ __forceinline__ typename MT<T>::x8 join(typename MT<T>::x4 a, typenam
   return r;
 }
 
+// ds_read_b64_tr_b16 as inline asm: invisible to hipcc's LDS-DMA alias
+// tracking, so no vmcnt(0) is inserted in front of it while a
+// global_load_lds into ANOTHER buffer is in flight.  The result is NOT
+// tracked either: the consumer must follow lds_wait() (lgkmcnt + a
+// sched_barrier so no MFMA is hoisted above the wait, CDNA guide rule 18).
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x4 tr_read_asm(const T* lds) {
+  typename MT<T>::x4 r;
+  const uint32_t a = (uint32_t)(uintptr_t)lds;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// The same with a compile-time byte offset folded into the instruction.
+template <int OFF, typename T>
+__device__ __forceinline__ typename MT<T>::x4 tr_read_imm(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  typename MT<T>::x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF));
+  return r;
+}
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Registers 8s..8s+7 of an fp32 accumulator -> operand fragment of k-step s.
 template <typename T>
 __device__ __forceinline__ typename MT<T>::x8 acc_frag(const f32x16& acc, int s) {
@@ -133,6 +169,19 @@ __device__ __forceinline__ int swz(int row) {
 template <int HD>
 __device__ __forceinline__ int sw_off(int row, int col) {
   return row * HD + (((col >> 3) ^ swz<HD>(row)) << 3) + (col & 7);
+}
+
+// Image (a) of CDNA guide T10 for [rows][HD] 16-bit tiles: 8-row x 32-column
+// (512-B) subtiles with a 2-bit XOR inside each 64-B row piece.  Byte offset
+// of 16-B chunk `ch` of row `row`.  Every 32x32x16 row read (ds_read_b128) and
+// transposed read (ds_read_b64_tr_b16) of it is conflict-free, and reads that
+// differ only in the k-step / d-tile / row-group differ by a lane-independent
+// constant (an instruction immediate), so a handful of address VGPRs serve a
+// whole tile.
+template <int HD>
+__device__ __forceinline__ int ia_off(int row, int ch) {
+  constexpr int RG = 8 * HD * 2;
+  return RG * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
 }  // namespace fa

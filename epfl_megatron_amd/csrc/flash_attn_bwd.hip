@@ -74,6 +74,8 @@ __global__ __launch_bounds__(256) void fa_delta_k(const AttnBwdParams P) {
     for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)g[e];
   }
   P.delta[t] = s;
+  P.ndelta[t] = -s;
+  P.lse2[t] = p.lse[t] * 1.4426950408889634f;
 }
 
 template <typename T, int HD, bool CAUSAL, int OCC, bool STAMP = false>
@@ -483,6 +485,396 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_k(const AttnBwdParams P) {
   }
 }
 
+// dK/dV, v2: the same per-wave math as fa_bwd_dkdv_k (4 waves x 32 keys, K/V
+// fragments and dK^T/dV^T accumulators register-resident), but each step
+// covers 64 query rows (two 32-row sub-slices: half the barriers per unit of
+// work) and the Q / dO / LSE / delta tiles arrive by LDS-DMA into a 2-deep
+// ring (issued one step ahead; the lane-linear image takes the sw_off swizzle
+// through the per-lane SOURCE address) — no staging registers and no
+// ds_write pass, which together cost more than the step's MFMAs in the
+// round-1 kernel (profiles/r1_fa_bwd_split.txt).  Transposed reads are inline
+// asm so hipcc does not drain the in-flight DMA in front of them.
+constexpr int BQ2 = 64;
+
+template <typename T, int HD, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) {
+  typedef typename MT<T>::x8 x8;
+  typedef typename MT<T>::x4 x4;
+  const AttnParams& p = P.f;
+  constexpr int KS = HD / 16, DT = HD / 32;
+  constexpr int ROWB = HD * 2;                   // bytes per Q / dO row
+  constexpr int RG = 8 * ROWB;                   // bytes per 8-row group (image (a))
+  constexpr int TILEB = BQ2 * ROWB;              // one Q (or dO) tile
+  constexpr int BUFB = 2 * TILEB + 2 * BQ2 * 4;  // Q, dO, lse2, -delta
+  constexpr int PIECES = TILEB / 1024, PPW = PIECES / 4;
+  static_assert(PIECES % 4 == 0, "pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, l4 = (lane >> 4) & 1;
+  const int nb = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+  const int r = p.nq / p.nkv;
+  const int off = p.sk - p.sq;
+  const int kbase = nb * BNK + wave * 32;
+  const int key = kbase + c;
+  const int key_c = key < p.sk ? key : p.sk - 1;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
+  const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
+
+  int q_first = 0;
+  if (CAUSAL) {
+    q_first = nb * BNK - off;
+    q_first = q_first < 0 ? 0 : (q_first / BQ2) * BQ2;
+  }
+  const int nsteps_q = p.sq > q_first ? (p.sq - q_first + BQ2 - 1) / BQ2 : 0;
+  const int nsteps = r * nsteps_q;
+
+  // LDS-DMA source offsets of this lane's pieces (image (a) through the source)
+  int srow[PPW], schunk[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int o = (wave * PPW + i) * 1024 + 16 * lane;
+    const int rem = o % RG, rem2 = rem % 512;
+    srow[i] = 8 * (o / RG) + rem2 / 64;
+    schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
+  }
+  auto prefetch = [&](int step, int buf) {
+    const int hh = step / nsteps_q;
+    const int q0 = q_first + (step - hh * nsteps_q) * BQ2;
+    const int head = g * r + hh;
+    const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)hh * p.q_sh;
+    const T* DO = (const T*)P.dout + (int64_t)b * p.o_sb + (int64_t)head * p.o_sh;
+    char* base = lds + buf * BUFB;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;
+      int qr = q0 + srow[i];
+      qr = qr < p.sq ? qr : p.sq - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(Q + (int64_t)qr * p.q_ss + schunk[i] * 8),
+                                       (__attribute__((address_space(3))) void*)(base + pc * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(DO + (int64_t)qr * p.o_ss + schunk[i] * 8),
+          (__attribute__((address_space(3))) void*)(base + TILEB + pc * 1024), 16, 0, 0);
+    }
+    if (wave < 2) {  // 64 rows x 4 B: one dword-wide piece each for lse2 and -delta
+      int qr = q0 + lane;
+      qr = qr < p.sq ? qr : p.sq - 1;
+      const int64_t rb = ((int64_t)b * p.nq + head) * p.sq;
+      const float* src = wave == 0 ? P.lse2 + rb + qr : P.ndelta + rb + qr;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(base + 2 * TILEB + wave * BQ2 * 4), 4, 0, 0);
+    }
+  };
+  if (nsteps > 0) prefetch(0, 0);
+
+  // loop-invariant LDS read offsets (the rest are immediates)
+  int rowb[2], trb[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    rowb[x] = RG * (c >> 3) + 64 * (c & 7) + 16 * ((2 * x + h) ^ ((c >> 2) & 3));
+    trb[x] = RG * x + 64 * (4 * h + tq) + 16 * ((2 * l4 + (tp >> 1)) ^ ((h + 2 * x) & 3)) +
+             8 * (tp & 1);
+  }
+  const int cstb = 2 * TILEB + 4 * (4 * h);
+
+  x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    kf[kk] = ld8(K + (int64_t)key_c * p.k_ss + kk * 16 + 8 * h);
+    vf[kk] = ld8(V + (int64_t)key_c * p.v_ss + kk * 16 + 8 * h);
+  }
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
+  __syncthreads();  // vmcnt(0) + barrier: step 0 landed
+
+  for (int step = 0; step < nsteps; ++step) {
+    const int hh = step / nsteps_q;
+    const int q0 = q_first + (step - hh * nsteps_q) * BQ2;
+    const int buf = step & 1;
+    if (step + 1 < nsteps) prefetch(step + 1, buf ^ 1);
+    const char* bb = lds + buf * BUFB;
+    const uint32_t trv0 = (uint32_t)(uintptr_t)(bb + trb[0]);
+    const uint32_t trv1 = (uint32_t)(uintptr_t)(bb + trb[1]);
+    static_for<BQ2 / 32>([&](auto s2c) {
+      constexpr int s2 = decltype(s2c)::value;
+      const char* qb = bb + s2 * 4 * RG;  // 32 rows = 4 row groups
+      const float* cst = reinterpret_cast<const float*>(bb + cstb) + 32 * s2;
+      const int q0s = q0 + 32 * s2;
+      f4 l24[4], nd4[4];
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        l24[rg] = *reinterpret_cast<const f4*>(cst + 8 * rg);
+        nd4[rg] = *reinterpret_cast<const f4*>(cst + BQ2 + 8 * rg);
+      }
+      // dP accumulator starts at -delta (row constant): dS = P * (dP - delta)
+      f32x16 dpacc = __builtin_shufflevector(__builtin_shufflevector(nd4[0], nd4[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                             __builtin_shufflevector(nd4[2], nd4[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                             0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      f32x16 sacc;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int o = rowb[kk & 1] + 512 * (kk >> 1);
+        const x8 qa = *reinterpret_cast<const x8*>(qb + o);
+        const x8 da = *reinterpret_cast<const x8*>(qb + TILEB + o);
+        if (kk == 0) {
+          sacc = mfma_vgpr0<T>(qa, kf[0]);
+          mfma_vgpr<T, 1>(dpacc, da, vf[0]);
+        } else {
+          mfma_vgpr<T>(sacc, qa, kf[kk]);
+          mfma_vgpr<T>(dpacc, da, vf[kk]);
+        }
+      }
+      x4 doa[2][DT][2], qta[2][DT][2];
+      static_for<2>([&](auto sc) {
+        static_for<DT>([&](auto dc) {
+          constexpr int o = s2 * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
+          doa[sc][dc][0] = tr_read_imm<TILEB + o, T>(trv0);
+          doa[sc][dc][1] = tr_read_imm<TILEB + o, T>(trv1);
+          qta[sc][dc][0] = tr_read_imm<o, T>(trv0);
+          qta[sc][dc][1] = tr_read_imm<o, T>(trv1);
+        });
+      });
+      mfma_drain();
+      const bool need_mask = (q0s + 32 > p.sq) || (kbase + 32 > p.sk) ||
+                             (CAUSAL && (kbase + 31 > q0s + off));
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -l24[i >> 2][i & 3]));
+      if (need_mask) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qr = q0s + acc_row(i, h);
+          const bool ok = (qr < p.sq) & (key < p.sk) & (!CAUSAL | (key <= qr + off));
+          sacc[i] = ok ? sacc[i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
+      lds_wait();  // the asm transposed reads above
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const x8 pf = acc_frag<T>(sacc, s);
+        const x8 sf = acc_frag<T>(dpacc, s);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          if (d == 0) mfma_agpr<T, 1>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
+          else mfma_agpr<T>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
+          mfma_agpr<T>(dk[d], join<T>(qta[s][d][0], qta[s][d][1]), sf);
+        }
+      }
+    });
+    __syncthreads();  // vmcnt(0) + barrier: step+1 landed, this step's reads retired
+  }
+
+  mfma_drain();
+  if (key < p.sk) {
+    T* DK = (T*)P.dk + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg + (int64_t)key * p.k_ss;
+    T* DV = (T*)P.dv + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + (int64_t)key * p.v_ss;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        x4 wk, wv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          wk[e] = (T)(dk[d][4 * rg + e] * p.scale);
+          wv[e] = (T)dv[d][4 * rg + e];
+        }
+        *reinterpret_cast<x4*>(DK + d * 32 + 8 * rg + 4 * h) = wk;
+        *reinterpret_cast<x4*>(DV + d * 32 + 8 * rg + 4 * h) = wv;
+      }
+    }
+  }
+}
+
+// dQ, v2: WAVES x 32 query rows of one head per workgroup (WAVES = 8: 512
+// threads sharing every K/V tile; two waves per SIMD), K/V double-buffered in
+// LDS with ONE barrier per 64-key tile (next tile's loads issued before the
+// MFMAs, written to the other buffer after them), flat grid with the query
+// blocks holding the most keys (causal) dispatched first.  Same math as
+// fa_bwd_dq_k.
+template <typename T, int HD, bool CAUSAL, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const AttnBwdParams P) {
+  typedef typename MT<T>::x8 x8;
+  typedef typename MT<T>::x4 x4;
+  const AttnParams& p = P.f;
+  constexpr int NT = WAVES * 64, BMW = WAVES * 32;
+  constexpr int KS = HD / 16, DT = HD / 32, CPR = HD / 8;
+  __shared__ __attribute__((aligned(16))) T lds[2 * 2 * KT * HD];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const int nqb = (p.sq + BMW - 1) / BMW;
+  const int nhb = p.nq * p.b;
+  const int lin = blockIdx.x;
+  const int qb = CAUSAL ? (nqb - 1 - lin / nhb) : lin / nhb;
+  const int head = (lin % nhb) % p.nq, b = (lin % nhb) / p.nq;
+  const int r = p.nq / p.nkv, g = head / r, hh = head - g * r;
+  const int off = p.sk - p.sq;
+  const int q0w = qb * BMW + wave * 32;
+  const int qrow = q0w + c;
+  const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)hh * p.q_sh;
+  const T* DO = (const T*)P.dout + (int64_t)b * p.o_sb + (int64_t)head * p.o_sh;
+  const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
+  const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
+
+  int kend = p.sk;
+  if (CAUSAL) {
+    const int last = qb * BMW + BMW + off;
+    kend = last < kend ? last : kend;
+  }
+  const int ntiles = kend > 0 ? (kend + KT - 1) / KT : 0;
+  int wtiles = ntiles;  // this wave's causal horizon
+  if (CAUSAL) {
+    const int wl = q0w + 32 + off;
+    const int wt = wl > 0 ? (wl + KT - 1) / KT : 0;
+    wtiles = wt < ntiles ? wt : ntiles;
+  }
+
+  // K / V tiles arrive by LDS-DMA (global_load_lds_dwordx4: lane-linear LDS
+  // image; the image-(a) layout (ia_off) is produced through the per-lane
+  // SOURCE address): no staging registers, no ds_write pass.  One 1-KiB
+  // piece per wave-instruction.  All LDS reads are base VGPR + immediate.
+  constexpr int ROWB = HD * 2, RG = 8 * ROWB, PIECES = KT * ROWB / 1024, PPW = PIECES / WAVES;
+  static_assert(PIECES % WAVES == 0, "pieces per wave");
+  int srow[PPW], schunk[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int o = (wave * PPW + i) * 1024 + 16 * lane;
+    const int rem = o % RG, rem2 = rem % 512;
+    srow[i] = 8 * (o / RG) + rem2 / 64;
+    schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
+  }
+  auto prefetch = [&](int t, int buf) {
+    char* kl = reinterpret_cast<char*>(lds + buf * 2 * KT * HD);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;
+      const int row = srow[i], chunk = schunk[i];
+      int kr = t * KT + row;
+      kr = kr < p.sk ? kr : p.sk - 1;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(K + (int64_t)kr * p.k_ss + chunk * 8),
+          (__attribute__((address_space(3))) void*)(kl + pc * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(V + (int64_t)kr * p.v_ss + chunk * 8),
+          (__attribute__((address_space(3))) void*)(kl + KT * ROWB + pc * 1024), 16, 0, 0);
+    }
+  };
+  if (ntiles > 0) prefetch(0, 0);
+
+  x8 qf[KS], df[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
+    df[kk] = ld8(DO + (int64_t)qrow_c * p.o_ss + kk * 16 + 8 * h);
+  }
+  const int64_t rb = ((int64_t)b * p.nq + head) * p.sq;
+  const float lse2 = p.lse[rb + qrow_c] * 1.4426950408889634f;
+  const float dlt = P.delta[rb + qrow_c];
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
+
+  int rowb[2], trb[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    rowb[x] = RG * (c >> 3) + 64 * (c & 7) + 16 * ((2 * x + h) ^ ((c >> 2) & 3));
+    trb[x] = RG * x + 64 * (4 * h + tq) + 16 * ((2 * ((lane >> 4) & 1) + (tp >> 1)) ^ ((h + 2 * x) & 3)) +
+             8 * (tp & 1);
+  }
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) prefetch(t + 1, buf ^ 1);
+    const char* kl = reinterpret_cast<const char*>(lds + buf * 2 * KT * HD);
+    const char* vl = kl + KT * ROWB;
+    const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
+    const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
+    if (t < wtiles) {
+      static_for<KT / 32>([&](auto subc) {
+        constexpr int sub = decltype(subc)::value;
+        const int kb = t * KT + sub * 32;
+        f32x16 sacc, dpacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dpacc[i] = -dlt;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int o = sub * 4 * RG + rowb[kk & 1] + 512 * (kk >> 1);
+          const x8 ka = *reinterpret_cast<const x8*>(kl + o);
+          const x8 va = *reinterpret_cast<const x8*>(vl + o);
+          if (kk == 0) {
+            sacc = mfma_vgpr0<T>(ka, qf[0]);
+            mfma_vgpr<T, 1>(dpacc, va, df[0]);
+          } else {
+            mfma_vgpr<T>(sacc, ka, qf[kk]);
+            mfma_vgpr<T>(dpacc, va, df[kk]);
+          }
+        }
+        mfma_drain();
+        const bool need_mask = (kb + 32 > p.sk) || (q0w + 32 > p.sq) ||
+                               (CAUSAL && kb + 31 > q0w + off);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -lse2));
+        if (need_mask) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kr = kb + acc_row(i, h);
+            const bool ok = (kr < p.sk) & (qrow < p.sq) & (!CAUSAL | (kr <= qrow + off));
+            sacc[i] = ok ? sacc[i] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = sacc[i] * dpacc[i];
+        static_for<2>([&](auto sc) {
+          const x8 sf = acc_frag<T>(sacc, decltype(sc)::value);
+          static_for<DT>([&](auto dc) {
+            constexpr int o = sub * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
+            const typename MT<T>::x4 k0 = tr_read_imm<o, T>(trv0);
+            const typename MT<T>::x4 k1 = tr_read_imm<o, T>(trv1);
+            lds_wait();
+            mfma_vgpr<T, 1>(dq[dc], join<T>(k0, k1), sf);
+          });
+        });
+      });
+    }
+    __syncthreads();  // vmcnt(0) + barrier: tile t+1 landed, tile t's reads retired
+  }
+
+  mfma_drain();
+  if (qrow < p.sq) {
+    T* DQ = (T*)P.dq + (int64_t)b * p.q_sb + (int64_t)qrow * p.q_ss + (int64_t)g * p.q_sg +
+            (int64_t)hh * p.q_sh;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (T)(dq[d][4 * rg + e] * p.scale);
+        *reinterpret_cast<x4*>(DQ + d * 32 + 8 * rg + 4 * h) = w;
+      }
+    }
+  }
+}
+
 template <typename T, int HD>
 void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
   static const int ablate = [] {
@@ -502,11 +894,24 @@ void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
     return e ? atoi(e) : 11;
   }();
   const bool kv2 = occ / 10 == 2, q2 = occ % 10 == 2;
+  // dQ kernel: EMA_FA_DQ = 1 (round-1 4-wave kernel) or 8 (8-wave, default)
+  static const int dqv = [] {
+    const char* e = getenv("EMA_FA_DQ");
+    return e ? atoi(e) : 8;
+  }();
+  const dim3 gq2(((p.sq + 255) / 256) * p.nq * p.b);
+  // dK/dV kernel: EMA_FA_DKDV = 1 (round-1 kernel) or 2 (64-row steps, LDS-DMA, default)
+  static const int kvv = [] {
+    const char* e = getenv("EMA_FA_DKDV");
+    return e ? atoi(e) : 2;
+  }();
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
-    if (kv2) hipLaunchKernelGGL((fa_bwd_dkdv_k<T, HD, C, 2>), gkv, dim3(256), 0, s, P);   \
+    if (kvv == 2) hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P); \
+    else if (kv2) hipLaunchKernelGGL((fa_bwd_dkdv_k<T, HD, C, 2>), gkv, dim3(256), 0, s, P); \
     else hipLaunchKernelGGL((fa_bwd_dkdv_k<T, HD, C, 1>), gkv, dim3(256), 0, s, P);       \
-    if (q2) hipLaunchKernelGGL((fa_bwd_dq_k<T, HD, C, 2>), gq, dim3(256), 0, s, P);       \
+    if (dqv == 8) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq2, dim3(512), 0, s, P); \
+    else if (q2) hipLaunchKernelGGL((fa_bwd_dq_k<T, HD, C, 2>), gq, dim3(256), 0, s, P);  \
     else hipLaunchKernelGGL((fa_bwd_dq_k<T, HD, C, 1>), gq, dim3(256), 0, s, P);          \
   }
   static const bool stamps = getenv("EMA_FA_STAMPS") != nullptr;

@@ -104,6 +104,8 @@ struct AttnBwdParams {
   void* dk;  // same strides as k
   void* dv;  // same strides as v
   float* delta;   // fp32 [b, nq, sq] workspace
+  float* ndelta;  // fp32 [b, nq, sq]: -delta (initial dP accumulator of the v2 kernels)
+  float* lse2;    // fp32 [b, nq, sq]: lse * log2(e)
   int ablate;     // profiling only (EMA_FA_ABLATE): bit 0 = no in-loop global prefetch
   uint64_t* stamps;  // diagnostic build only (EMA_FA_STAMPS)
 };
