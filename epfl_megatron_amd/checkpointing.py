@@ -28,7 +28,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import global_vars
+from . import ckpt_pickle, global_vars
 from .parallel import state
 from .parallel.tensor.random import get_cuda_rng_tracker
 from .models import enums as _enums
@@ -54,6 +54,14 @@ def _safe_globals():
     for e in _enums.ALL_ENUMS:
         allow.append(e)
         allow.append((e, f"megatron.model.enums.{e.__name__}"))
+    # very old checkpoints pickled their loss scaler objects (reference
+    # checkpointing.py:457-468 remaps these module paths)
+    from .fp16_deprecated import loss_scaler as _ls
+    for cls in (_ls.LossScaler, _ls.DynamicLossScaler):
+        allow.append(cls)
+        for mod in ("fp16.loss_scaler", "megatron.fp16.loss_scaler",
+                    "megatron.fp16_deprecated.loss_scaler"):
+            allow.append((cls, f"{mod}.{cls.__name__}"))
     try:
         import numpy.core.multiarray as ma
         allow += [ma._reconstruct, np.ndarray, np.dtype, type(np.dtype(np.uint32))]
@@ -62,10 +70,35 @@ def _safe_globals():
     return allow
 
 
-def safe_load(path, map_location="cpu"):
+def safe_load(path, map_location="cpu", mmap=False):
     """``torch.load(weights_only=True)`` with our allow-list."""
     with torch.serialization.safe_globals(_safe_globals()):
-        return torch.load(path, map_location=map_location, weights_only=True)
+        return torch.load(path, map_location=map_location, weights_only=True, mmap=mmap)
+
+
+class DPPeerLoader:
+    """Reads the distributed-optimizer ``optim.pt`` of any DP rank of this
+    (TP, PP) rank (``mp_rank_TT[_PPP]_RRR/optim.pt``, reference
+    ``checkpointing.py:107-140``).  The optimizer state there is sharded by the
+    reference buffer layout, so a rank gathers its own ranges from all of them
+    — which also makes a load at a different DP size or bucket size work."""
+
+    def __init__(self, load_dir, iteration, release):
+        self.load_dir, self.iteration, self.release = load_dir, iteration, release
+        model_name, _ = get_checkpoint_names(load_dir, iteration, True, release)
+        self.prefix = os.path.dirname(model_name)
+
+    def path(self, r):
+        return self.prefix + f"_{r:03d}/optim.pt"
+
+    def num_ranks(self):
+        n = 0
+        while os.path.exists(self.path(n)):
+            n += 1
+        return n
+
+    def __call__(self, r):
+        return safe_load(self.path(r), mmap=True)["optimizer"]
 
 
 def check_checkpoint_args(checkpoint_args):
@@ -232,7 +265,8 @@ def save_checkpoint(iteration, model, optimizer, opt_param_scheduler):
     def _write(items):
         for name, obj in items:
             ensure_directory_exists(name)
-            torch.save(obj, name)
+            # enums pickled under megatron.model.enums: the reference loads these files
+            torch.save(obj, name, pickle_module=ckpt_pickle.pickle_module)
 
     if args.async_save:
         items = [(n, _to_host(o)) for n, o in writes]
@@ -269,8 +303,11 @@ def _load_base_checkpoint(load_dir, use_distributed_optimizer, rank0=False):
         print_rank_0(f" loading checkpoint from {load_dir} at iteration {iteration}")
     model_sd = safe_load(model_name)
     optim_sd = None
-    if use_distributed_optimizer and not rank0 and os.path.exists(optim_name):
-        optim_sd = safe_load(optim_name)
+    if use_distributed_optimizer and not rank0:
+        if not os.path.exists(optim_name):  # written at a smaller DP size
+            optim_name = DPPeerLoader(load_dir, iteration, release).path(0)
+        if os.path.exists(optim_name):
+            optim_sd = safe_load(optim_name, mmap=True)
     elif not use_distributed_optimizer:
         optim_sd = model_sd
     return model_sd, optim_sd, release
@@ -328,14 +365,48 @@ def load_args_from_checkpoint(args, load_arg="load"):
     return args, ck
 
 
+def _transpose_first_dim(t, num_splits, num_splits_first, heads, head_dim):
+    """Row-block reorder of a fused QKV (or KV) weight/bias to the 2.0+ layout
+    ``[np, num_splits, hn, ...]`` (reference ``checkpointing.py:340-376``)."""
+    shape = t.shape
+    if num_splits_first:   # [num_splits * np * hn, ...] (checkpoint_version 0)
+        t = t.view(num_splits, heads, head_dim, *shape[1:]).transpose(0, 1)
+    else:                  # [np * hn * num_splits, ...] (checkpoint_version 1.0)
+        t = t.view(heads, head_dim, num_splits, *shape[1:]).transpose(1, 2)
+    return t.contiguous().view(*shape)
+
+
 def fix_query_key_value_ordering(model, checkpoint_version):
-    """Checkpoints older than 2.0 stored QKV in another row order (no GQA)."""
+    """Checkpoints older than 2.0 stored fused QKV rows as [3, np, hn] (v0) or
+    [np, hn, 3] (v1.0); migrate them in place to the [np, 3, hn] layout
+    (reference ``checkpointing.py:379-411``; GQA/MQA weights never had the old
+    layouts and are left alone)."""
     if checkpoint_version >= 2.0:
         return
+    if checkpoint_version not in (0, 1.0):
+        raise ValueError(f"Invalid checkpoint version {checkpoint_version}.")
+    if isinstance(model, list):
+        if len(model) != 1:
+            raise AssertionError("QKV migration supports a single model chunk")
+        model = model[0]
+    while hasattr(model, "module"):
+        model = model.module
+    args = global_vars.get_args()
+    attn = model.language_model.encoder.layers[0].self_attention
+    heads = attn.num_attention_heads_per_partition
+    head_dim = attn.hidden_size_per_attention_head
+    first = checkpoint_version == 0
     for name, param in model.named_parameters():
-        if name.endswith(("query_key_value.weight", "query_key_value.bias")):
-            print_rank_0(f" warning: checkpoint version {checkpoint_version} QKV layout not "
-                         f"migrated for {name}")
+        if name.endswith((".query_key_value.weight", ".query_key_value.bias")):
+            if args.num_attention_heads_kv != args.num_attention_heads:
+                continue
+            with torch.no_grad():
+                param.copy_(_transpose_first_dim(param.data, 3, first, heads, head_dim))
+        elif name.endswith((".key_value.weight", ".key_value.bias")):
+            with torch.no_grad():
+                param.copy_(_transpose_first_dim(param.data, 2, first, heads, head_dim))
+    print_rank_0(f" succesfully fixed query-key-values ordering for checkpoint version "
+                 f"{checkpoint_version}")
 
 
 def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", strict=True):
@@ -367,7 +438,12 @@ def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", stri
     if not release and not args.finetune and not args.no_load_optim:
         try:
             if optimizer is not None and optim_sd is not None and "optimizer" in optim_sd:
-                optimizer.load_state_dict(optim_sd["optimizer"])
+                if args.use_distributed_optimizer:
+                    it, rel = _read_meta_local(get_checkpoint_tracker_filename(load_dir))
+                    optimizer.load_state_dict(optim_sd["optimizer"],
+                                              dp_peer_loader=DPPeerLoader(load_dir, it, rel))
+                else:
+                    optimizer.load_state_dict(optim_sd["optimizer"])
             if opt_param_scheduler is not None and "opt_param_scheduler" in model_sd:
                 opt_param_scheduler.load_state_dict(model_sd["opt_param_scheduler"])
         except KeyError as e:

@@ -12,6 +12,7 @@ import os
 
 import torch
 
+from .. import ckpt_pickle
 from ..checkpointing import _safe_globals
 from .shard import merge_shards, split_full
 
@@ -101,7 +102,8 @@ def save_sharded(ckpt_dir, full, args, tp=1, pp=1, iteration="release", padded_v
             model = _own(shards[p][r])
             torch.save({"iteration": iteration if iteration == "release" else int(iteration),
                         "model": model, "checkpoint_version": checkpoint_version,
-                        "args": args}, os.path.join(d, "model_optim_rng.pt"))
+                        "args": args}, os.path.join(d, "model_optim_rng.pt"),
+                       pickle_module=ckpt_pickle.pickle_module)
     with open(os.path.join(ckpt_dir, TRACKER), "w") as f:
         f.write(str(iteration))
     return base

@@ -66,7 +66,13 @@ class MegatronModule(torch.nn.Module):
                 self.word_embeddings.weight.fill_(0)
             self.word_embeddings.weight.shared = True
         if not state.is_pipeline_first_stage(ignore_virtual=True) and self.pre_process:
+            # decoder stage of a split encoder/decoder pipeline: its embeddings
+            # are replicas of the first stage's (summed over the embedding /
+            # position-embedding groups).  Marked shared so the grad norm counts
+            # them once (the reference counts them twice).
             self.language_model.embedding.zero_parameters()
+            for prm in self.language_model.embedding.parameters():
+                prm.shared = True
         if not dist.is_initialized():
             return
         if state.is_rank_in_embedding_group():

@@ -116,8 +116,11 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
                 emb = [ranks[0], ranks[-1]]
                 pos = [ranks[0]]
                 split = pipeline_model_parallel_split_rank
-                if split is not None and ranks[split] not in emb:
-                    emb = [ranks[0], ranks[split], ranks[-1]]
+                if split is not None:
+                    if ranks[split] not in emb:
+                        emb = [ranks[0], ranks[split], ranks[-1]]
+                    # independent of the embedding group: the decoder's first
+                    # stage may also be the last one (e.g. PP=2, split 1)
                     if ranks[split] not in pos:
                         pos = [ranks[0], ranks[split]]
             else:

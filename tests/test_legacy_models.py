@@ -298,3 +298,55 @@ def test_classification_and_multiple_choice_heads(tmp_path):
     argv = BERT_TINY + ["--vocab_file", _vocab_file(tmp_path)]
     out = run_dist(_heads_worker, 1, argv)[0]
     assert out == ((4, 3), (2, 2), ["classification_head", "language_model"])
+
+
+def _t5_pp_worker(rank, world, argv, steps=3):
+    """T5 steps with every weight filled from its global name (same values at
+    any PP split), so PP=2 with a split rank must reproduce PP=1."""
+    import importlib
+    mod = importlib.import_module("pretrain_t5")
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.initialize import initialize_megatron
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.optim import get_megatron_optimizer
+    from epfl_megatron_amd.parallel import state
+    from epfl_megatron_amd.training import (get_model, _get_optimizer_param_scheduler,
+                                            build_train_valid_test_data_iterators, train_step)
+    from test_parallel_equivalence import _deterministic_init
+    initialize_megatron(None, {}, args_list=argv)
+    args = get_args()
+    model = get_model(mod.model_provider, ModelType.encoder_and_decoder)
+    _deterministic_init(model, args)
+    opt = get_megatron_optimizer(model)
+    sched = _get_optimizer_param_scheduler(opt)
+    args.iteration = 0
+    it, _, _ = build_train_valid_test_data_iterators(mod.train_valid_test_datasets_provider, args)
+    losses = []
+    for _ in range(steps):
+        out = train_step(mod.forward_step, it, model, opt, sched, args)
+        args.consumed_train_samples += args.global_batch_size
+        if out[0]:
+            losses.append((float(out[0]["lm loss"]), float(out[2])))
+    return losses if state.is_pipeline_last_stage(ignore_virtual=True) else None
+
+
+def test_t5_pipeline_split_rank(tmp_path):
+    """Encoder on stage 0, decoder on stage 1 (--pipeline_model_parallel_split_rank,
+    reference schedules.py:505-535, parallel_state.py:367-403): shared word
+    embeddings summed over the embedding group {0, 1}, position embeddings over
+    the position-embedding group, losses equal to the single-stage run."""
+    from dist_utils import run_dist
+    argv = [a for a in BERT_TINY]
+    i = argv.index("--seq_length")
+    argv[i:i + 2] = ["--encoder_seq_length", "32"]
+    argv += ["--decoder_seq_length", "16", "--vocab_extra_ids", "10", "--data_path",
+             _write_corpus(tmp_path), "--vocab_file", _vocab_file(tmp_path),
+             "--micro_batch_size", "1"]
+    one = [r for r in run_dist(_t5_pp_worker, 1, argv) if r][0]
+    two = [r for r in run_dist(_t5_pp_worker, 2, argv + [
+        "--pipeline_model_parallel_size", "2", "--pipeline_model_parallel_split_rank", "1"])
+        if r][0]
+    assert len(one) == len(two) == 3
+    for (l0, g0), (l1, g1) in zip(one, two):
+        assert abs(l0 - l1) < 2e-5 * max(1.0, abs(l0)), (one, two)
+        assert abs(g0 - g1) < 1e-4 * max(1.0, abs(g0)), (one, two)

@@ -14,8 +14,10 @@ from pathlib import Path
 
 import torch
 
+
 sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), os.path.pardir)))
 
+from epfl_megatron_amd import ckpt_pickle  # noqa: E402
 from epfl_megatron_amd.checkpointing import safe_load  # noqa: E402
 from epfl_megatron_amd.convert.qkv import permute_qkv  # noqa: E402,F401
 
@@ -48,7 +50,8 @@ def update_checkpoint(input_dir: Path, output_dir: Path, overwrite_ok=False, rev
                     if re.match(rf"^layers\.\d+\.{attn}\.query_key_value\.weight$", name):
                         states[name] = permute_qkv(states[name], a.hidden_size,
                                                    a.num_attention_heads, n_kv, revert=revert)
-            torch.save(ck, output_dir / sub / shard.name / f.name)
+            torch.save(ck, output_dir / sub / shard.name / f.name,
+                       pickle_module=ckpt_pickle.pickle_module)
 
 
 if __name__ == "__main__":
