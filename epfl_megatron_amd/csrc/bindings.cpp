@@ -507,6 +507,54 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 
+// ---------------------------------------------------------------- bias-dropout-add
+at::Tensor bias_dropout_add_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& x2,
+                                const c10::optional<at::Tensor>& bias, const at::Tensor& res,
+                                double p, int64_t seed, int64_t offset) {
+  check_gpu(x, "x");
+  check_gpu(res, "residual");
+  TORCH_CHECK(x.is_contiguous() && res.is_contiguous(), "x / residual must be contiguous");
+  TORCH_CHECK(x.sizes() == res.sizes() && x.scalar_type() == res.scalar_type(), "x / residual mismatch");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "bf16/fp16 only");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout probability must be in [0, 1)");
+  const int64_t h = x.size(-1);
+  TORCH_CHECK(h % 8 == 0 && x.numel() % 8 == 0, "hidden size must be a multiple of 8");
+  const void* x2p = nullptr;
+  if (x2.has_value() && x2->defined()) {
+    TORCH_CHECK(x2->sizes() == x.sizes() && x2->is_contiguous() &&
+                x2->scalar_type() == x.scalar_type(), "x2 must match x");
+    check_vec_aligned(*x2, "x2");
+    x2p = x2->data_ptr();
+  }
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() == h && bias->is_contiguous() && bias->scalar_type() == x.scalar_type(),
+                "bias must be [h] of x's dtype");
+    check_vec_aligned(*bias, "bias");
+    bp = bias->data_ptr();
+  }
+  auto out = at::empty_like(x);
+  check_vec_aligned(x, "x");
+  check_vec_aligned(res, "residual");
+  check_vec_aligned(out, "out");
+  if (x.numel() > 0)
+    ema::bias_dropout_add_fwd(x.data_ptr(), x2p, bp, res.data_ptr(), out.data_ptr(), x.numel(), h,
+                              (float)p, (uint64_t)seed, (uint64_t)offset, dtype_code(x), cur_stream());
+  return out;
+}
+
+at::Tensor bias_dropout_add_bwd(const at::Tensor& dout, double p, int64_t seed, int64_t offset) {
+  check_gpu(dout, "dout");
+  TORCH_CHECK(dout.is_contiguous() && dout.numel() % 8 == 0, "dout must be contiguous, numel % 8 == 0");
+  TORCH_CHECK(p > 0.0 && p < 1.0, "dropout probability must be in (0, 1)");
+  auto dx = at::empty_like(dout);
+  check_vec_aligned(dout, "dout");
+  if (dout.numel() > 0)
+    ema::bias_dropout_add_bwd(dout.data_ptr(), dx.data_ptr(), dout.numel(), (float)p, (uint64_t)seed,
+                              (uint64_t)offset, dtype_code(dout), cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- wgrad GEMM
 bool wgrad_supported(int64_t M, int64_t N, int64_t K) { return ema::wgrad_supported(M, N, K); }
 
@@ -589,6 +637,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chunked_sumsq", &chunked_sumsq);
   m.def("flat_adam", &flat_adam);
   m.def("opt_prep", &opt_prep);
+  m.def("bias_dropout_add_fwd", &bias_dropout_add_fwd);
+  m.def("bias_dropout_add_bwd", &bias_dropout_add_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("transpose16", &transpose16);

@@ -81,6 +81,15 @@ void opt_prep(const float* norm_sq, const float* inv_scale, float clip, float* s
 void flat_adam(float* master, void* model_out, int model_dt, const float* grad, float* m,
                float* v, const int64_t* table, int n_chunks, const AdamArgs& a, hipStream_t s);
 
+// ---- dropout.hip --------------------------------------------------------------------------
+// out = res + dropout(x [+ x2] [+ bias[col]]), Philox-4x32-10 keyed by (seed, offset);
+// n % 8 == 0, h % 8 == 0 (bias length).  bwd: dx = dout * mask / (1 - p), mask regenerated.
+void bias_dropout_add_fwd(const void* x, const void* x2, const void* bias, const void* res,
+                          void* out, int64_t n, int64_t h, float p, uint64_t seed, uint64_t offset,
+                          int dt, hipStream_t s);
+void bias_dropout_add_bwd(const void* dout, void* dx, int64_t n, float p, uint64_t seed,
+                          uint64_t offset, int dt, hipStream_t s);
+
 // ---- flash_attn_fwd.hip / flash_attn_bwd.hip -------------------------------------------------
 struct AttnParams {
   const void* q;

@@ -28,6 +28,7 @@ from .. import global_vars
 from ..parallel import state
 from ..parallel.buffers import divide, make_viewless_tensor
 from ..parallel import tensor as tp
+from ..ops.dropout import bias_dropout_add
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm
 from ..ops.rope import rope_table, apply_rope_ref
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func
@@ -344,15 +345,21 @@ class ParallelTransformerLayer(MegatronModule):
             self.post_inter_attention_layernorm = _make_norm(args)
         self.mlp = ParallelMLP(init_method, output_layer_init_method, args, world_size)
 
-    def _add(self, x, bias, residual, make_viewless=False):
-        if bias is not None:
-            x = x + bias
-        p = self.hidden_dropout if self.training else 0.0
-        if p > 0.0:
-            x = F.dropout(x, p=p, training=True)
-        if self.drop_path is not None:
-            x = self.drop_path(x)
-        out = residual + x
+    def _add(self, x, bias, residual, make_viewless=False, x2=None):
+        """residual + dropout(x [+ x2] [+ bias]): one fused HIP pass on the GPU
+        (``ops.dropout``, Philox-consistent with the TP RNG tracker); ``x2`` is
+        the Falcon parallel block's attention output."""
+        if self.drop_path is None:
+            out = bias_dropout_add(x, bias, residual, self.hidden_dropout, self.training, x2=x2)
+        else:
+            if x2 is not None:
+                x = x + x2
+            if bias is not None:
+                x = x + bias
+            p = self.hidden_dropout if self.training else 0.0
+            if p > 0.0:
+                x = F.dropout(x, p=p, training=True)
+            out = residual + self.drop_path(x)
         if make_viewless:
             out = make_viewless_tensor(out, requires_grad=out.requires_grad, keep_graph=True)
         return out
@@ -407,8 +414,9 @@ class ParallelTransformerLayer(MegatronModule):
             ln_in = self._add(attn_out, attn_bias, residual)
             ln_out = self.post_inter_attention_layernorm(ln_in)
         mlp_out, mlp_bias = self.mlp(ln_out)
-        if self.parallel_attn:
-            mlp_out = mlp_out + attn_out
+        if self.parallel_attn:  # Falcon: residual + dropout(mlp + attn) in one pass
+            out = self._add(mlp_out, mlp_bias, residual, make_viewless=True, x2=attn_out)
+            return self.output_layernorm(out)
         elif self.apply_residual_connection_post_layernorm:
             residual = ln_out
         else:

@@ -486,3 +486,58 @@ def test_flash_attention_bwd_kv_longer():
     _close(q.grad, qr.grad, 5e-2, 5e-2, "dq (sk > sq)")
     _close(k.grad, kr.grad, 5e-2, 5e-2, "dk (sk > sq)")
     _close(v.grad, vr.grad, 5e-2, 5e-2, "dv (sk > sq)")
+
+
+# ------------------------------------------------------ fused bias-dropout-add
+def test_bias_dropout_add_mask_bit_exact():
+    """GPU mask == the NumPy Philox-4x32-10 transcription (known-answer checked
+    on CPU), output == residual + where(mask, (x + x2 + bias) / (1 - p), 0)."""
+    from epfl_megatron_amd.ops._ext import ext
+    from epfl_megatron_amd.ops.dropout import philox_keep_mask
+    torch.manual_seed(3)
+    s, b, h, p = 37, 3, 256, 0.3
+    x, x2, r = (torch.randn(s, b, h, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    bias = torch.randn(h, device=DEV, dtype=torch.bfloat16)
+    seed, offset = 0x1234ABCD5678, 4096
+    out = ext().bias_dropout_add_fwd(x, x2, bias, r, p, seed, offset)
+    keep = torch.from_numpy(philox_keep_mask(x.numel(), p, seed, offset)).view(s, b, h).to(DEV)
+    ref = r.float() + torch.where(keep, (x.float() + x2.float() + bias.float()) / (1 - p),
+                                  torch.zeros((), device=DEV))
+    _close(out, ref, 2e-2, 2e-2, "bias_dropout_add fwd")
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    dout = torch.randn_like(x)
+    dx = ext().bias_dropout_add_bwd(dout, p, seed, offset)
+    _close(dx, torch.where(keep, dout.float() / (1 - p), torch.zeros((), device=DEV)), 1e-2,
+           1e-2, "bias_dropout_add bwd")
+
+
+def test_bias_dropout_add_autograd_and_rng_stream():
+    """Through the op: grads (dx = dx2 = mask*dout/(1-p), dbias = sum, dres = dout);
+    consecutive calls draw fresh masks; re-seeding reproduces them; the TP RNG
+    tracker's fork gives a different stream (sequence-parallel dropout)."""
+    from epfl_megatron_amd.ops.dropout import bias_dropout_add
+    from epfl_megatron_amd.parallel.tensor.random import get_cuda_rng_tracker
+    torch.manual_seed(4)
+    x = torch.randn(64, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn_like(x, requires_grad=True)
+    bias = torch.randn(128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    torch.cuda.manual_seed(11)
+    y1 = bias_dropout_add(x, bias, r, 0.25, True)
+    y2 = bias_dropout_add(x, bias, r, 0.25, True)
+    assert not torch.equal(y1, y2)
+    torch.cuda.manual_seed(11)
+    assert torch.equal(bias_dropout_add(x, bias, r, 0.25, True), y1)
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    keep = (y1 - r).detach().float().abs() > 0
+    dx = torch.where(keep, g.float() / 0.75, torch.zeros((), device=DEV))
+    _close(x.grad, dx, 2e-2, 2e-2, "dx")
+    _close(r.grad, g.float(), 0, 0, "dres")
+    _close(bias.grad, dx.view(-1, 128).sum(0), 5e-2, 5e-2, "dbias")
+    tracker = get_cuda_rng_tracker()
+    tracker.reset()
+    tracker.add("model-parallel-rng", 999)
+    torch.cuda.manual_seed(11)
+    with tracker.fork():
+        y3 = bias_dropout_add(x, bias, r, 0.25, True)
+    assert not torch.equal(y3, y1)

@@ -363,3 +363,28 @@ def test_checkpoint_resume_matches_uninterrupted(tmp_path):
         assert s[1] == r[1] == 8 and s[3] == r[3] == 8  # samples consumed / scheduled
         torch.testing.assert_close(s[2], r[2], atol=1e-6, rtol=1e-6)
     assert (tmp_path / "b" / "latest_checkpointed_iteration.txt").read_text() == "4"
+
+
+# ------------------------------------------------- Philox (fused dropout)
+def test_philox_known_answers():
+    """Random123 philox4x32-10 known-answer vectors: the NumPy transcription the
+    GPU dropout mask is checked against must be the real generator."""
+    import numpy as np
+    from epfl_megatron_amd.ops.dropout import _philox
+    kat = [((0, 0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((2**64 - 1, 2**64 - 1, 2**64 - 1), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x85a308d3243f6a88, 0x0370734413198a2e, 0x299f31d0a4093822),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for (ctr, off, key), want in kat:
+        got = _philox(np.array([ctr], dtype=np.uint64), off, key)
+        assert tuple(int(v[0]) for v in got) == want
+
+
+def test_bias_dropout_add_cpu_path():
+    from epfl_megatron_amd.ops.dropout import bias_dropout_add
+    torch.manual_seed(0)
+    x, r, b = torch.randn(64, 32), torch.randn(64, 32), torch.randn(32)
+    assert torch.allclose(bias_dropout_add(x, b, r, 0.3, False), r + x + b)
+    y = bias_dropout_add(x, b, r, 0.5, True, x2=x)
+    kept = ((y - r).abs() > 1e-6).float().mean().item()
+    assert 0.4 < kept < 0.6
