@@ -110,6 +110,36 @@ def build_dedup(force=False):
     return out
 
 
+SANITIZERS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def build_sanitized(kind, out_dir):
+    """Host-sanitizer harness: ``data_helpers.cpp`` + ``dedup.cpp`` as embedded
+    pybind11 modules linked with libpython into one executable
+    (``csrc/sanitize_main.cpp``), instrumented with ``kind`` in
+    :data:`SANITIZERS`.  The sanitizer runtime lives in the executable, so
+    nothing is preloaded.  CPU code only (no GPU sanitizer on this pool)."""
+    import pybind11
+    os.makedirs(out_dir, exist_ok=True)
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-pthread",
+             "-DEMA_EMBEDDED", "-I", pybind11.get_include(),
+             "-I", sysconfig.get_paths()["include"]] + SANITIZERS[kind]
+    objs = []
+    for src in ("data_helpers.cpp", "dedup.cpp", "sanitize_main.cpp"):
+        o = os.path.join(out_dir, f"{kind}_{src}.o")
+        _run(["g++", "-c"] + flags + [os.path.join(CSRC, src), "-o", o])
+        objs.append(o)
+    exe = os.path.join(out_dir, f"helpers_{kind}")
+    libdir = sysconfig.get_config_var("LIBDIR")
+    ver = sysconfig.get_config_var("LDVERSION")
+    _run(["g++"] + SANITIZERS[kind] + ["-pthread", "-o", exe] + objs +
+         [f"-L{libdir}", f"-lpython{ver}", "-ldl", "-lm", f"-Wl,-rpath,{libdir}"])
+    return exe
+
+
 def build_all(force=False, jobs=None):
     build_dedup(force)
     h = build_data_helpers(force)

@@ -26,7 +26,7 @@ __device__ __forceinline__ T from_f(float x) { return (T)x; }
 
 // 16-byte vector of T.
 template <typename T>
-struct V16 {
+struct alignas(16) V16 {
   static constexpr int N = 16 / sizeof(T);
   T v[N];
 };

@@ -10,6 +10,9 @@
 //   block_mapping : ICT evidence blocks (first sentence, end sentence, doc, block id).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#ifdef EMA_EMBEDDED
+#include <pybind11/embed.h>
+#endif
 
 #include <algorithm>
 #include <cmath>
@@ -296,7 +299,12 @@ py::array block_mapping(py::array_t<int64_t, py::array::c_style | py::array::for
 
 }  // namespace
 
+// EMA_EMBEDDED: linked into the host-sanitizer harness (csrc/sanitize_main.cpp)
+#ifdef EMA_EMBEDDED
+PYBIND11_EMBEDDED_MODULE(_helpers, m) {
+#else
 PYBIND11_MODULE(_helpers, m) {
+#endif
   m.doc() = "dataset index builders";
   m.def("sample_index", &sample_index);
   m.def("blend_indices", &blend_indices);

@@ -13,6 +13,9 @@
 // reference's `range(0, len(text) - char_ngram)` (the last window is skipped).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#ifdef EMA_EMBEDDED
+#include <pybind11/embed.h>
+#endif
 #include <pybind11/stl.h>
 
 #include <algorithm>
@@ -135,7 +138,12 @@ double jaccard(const std::string& a, const std::string& b, int char_ngram, int m
 
 }  // namespace
 
+// EMA_EMBEDDED: linked into the host-sanitizer harness (csrc/sanitize_main.cpp)
+#ifdef EMA_EMBEDDED
+PYBIND11_EMBEDDED_MODULE(_dedup, m) {
+#else
 PYBIND11_MODULE(_dedup, m) {
+#endif
   m.doc() = "MinHash / LSH / shingle-Jaccard kernels for corpus de-duplication";
   m.def("minhash", &minhash, py::arg("texts"), py::arg("seeds"), py::arg("char_ngram") = 5,
         py::arg("threads") = 8);

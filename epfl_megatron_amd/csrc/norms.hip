@@ -108,6 +108,16 @@ __device__ __forceinline__ void load_row(RowRegs<T, VPL>& rr, const T* __restric
   }
 }
 
+// w reads as one LLVM vector load.  Through the V16 struct, the DW+FULL
+// variants had SROA slice each 16-B read into u16/b64/u16/b32 pieces (4 LDS ops,
+// 2-byte aligned -> bank conflicts); a native vector type cannot be sliced.
+template <typename T>
+using lvec = T __attribute__((ext_vector_type(16 / sizeof(T))));
+template <typename T>
+__device__ __forceinline__ lvec<T> lds_ld16(const T* p) {
+  return *static_cast<const lvec<T>*>(__builtin_assume_aligned(p, 16));
+}
+
 template <typename T, int VPL, bool DW, bool FULL, bool DRES>
 __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T, VPL>& nxt,
                                             int64_t nrow, const T* __restrict__ x,
@@ -122,22 +132,22 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
   for (int i = 0; i < VPL; ++i) {
     const int vi = lane + i * 64;
     if (FULL || vi < nvec) {
-      const V16<T> wv = *reinterpret_cast<const V16<T>*>(w_lds + vi * N);
+      const lvec<T> wv = lds_ld16(w_lds + vi * N);
       float4 a[N / 4];
       if (DW) {
 #pragma unroll
-        for (int q = 0; q < N / 4; ++q) a[q] = *reinterpret_cast<const float4*>(acc + vi * N + 4 * q);
+        for (int q = 0; q < N / 4; ++q) a[q] = *reinterpret_cast<const float4*>(acc + q * nvec * 4 + vi * 4);
       }
 #pragma unroll
       for (int e = 0; e < N; ++e) {
         const float xh = to_f(rr.x[i].v[e]) * r;
         const float g = to_f(rr.g[i].v[e]);
-        dot += g * to_f(wv.v[e]) * xh;
+        dot += g * to_f(wv[e]) * xh;
         if (DW) reinterpret_cast<float*>(a)[e] += g * to_f(from_f<T>(xh));
       }
       if (DW) {
 #pragma unroll
-        for (int q = 0; q < N / 4; ++q) *reinterpret_cast<float4*>(acc + vi * N + 4 * q) = a[q];
+        for (int q = 0; q < N / 4; ++q) *reinterpret_cast<float4*>(acc + q * nvec * 4 + vi * 4) = a[q];
       }
     }
   }
@@ -158,12 +168,12 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
   for (int i = 0; i < VPL; ++i) {
     const int vi = lane + i * 64;
     if (FULL || vi < nvec) {
-      const V16<T> wv = *reinterpret_cast<const V16<T>*>(w_lds + vi * N);
+      const lvec<T> wv = lds_ld16(w_lds + vi * N);
       V16<T> o;
 #pragma unroll
       for (int e = 0; e < N; ++e) {
         const float xh = to_f(rr.x[i].v[e]) * r;
-        float v = r * (to_f(rr.g[i].v[e]) * to_f(wv.v[e]) - xh * dot);
+        float v = r * (to_f(rr.g[i].v[e]) * to_f(wv[e]) - xh * dot);
         if (DRES) v += to_f(rv[i].v[e]);
         o.v[e] = from_f<T>(v);
       }
@@ -174,7 +184,11 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
 
 // LDS: w (H x T) then, with DW, one private fp32 dW row per wave (4 x H x 4 B;
 // H <= 4096 -> <= 72 KB per workgroup).  Keeping dW in VGPRs next to the two
-// row buffers pinned the kernel at 1 wave/SIMD.
+// row buffers pinned the kernel at 1 wave/SIMD.  The dW row is stored as N/4
+// planes of float4 indexed [q][vi], so a wave's ds_read/write_b128 of it is 64
+// consecutive 16-B slots (conflict-free; the natural [vi][q] order put lanes 32
+// bytes apart: 2-way conflicts, 4.3 conflict cycles per LDS instruction in
+// profiles/r1_llama7b_pmc_step.csv).
 template <typename T, int VPL, bool DW, bool FULL, bool DRES>
 __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __restrict__ dy,
                                                         const T* __restrict__ x,
@@ -192,9 +206,14 @@ __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __re
   const int64_t nwaves = (int64_t)gridDim.x * kWaves;
   const int nvec = H / N;
   T* w_lds = reinterpret_cast<T*>(dyn_lds);
-  float* acc = dyn_lds + (H * sizeof(T) + 15) / 16 * 4 + (threadIdx.x >> 6) * H;
+  // H is a multiple of N (>= 8), so every wave's dW row starts 16-B aligned;
+  // telling the compiler keeps the accesses ds_read/write_b128 (it otherwise
+  // falls back to ds_read2_b64 and 2-byte pieces for w).
+  float* acc = static_cast<float*>(__builtin_assume_aligned(
+      dyn_lds + (H * sizeof(T) + 15) / 16 * 4 + (threadIdx.x >> 6) * H, 16));
   for (int j = threadIdx.x; j < nvec; j += 256)
-    *reinterpret_cast<V16<T>*>(w_lds + j * N) = ld16(w + j * N);
+    *static_cast<uint4*>(__builtin_assume_aligned(w_lds + j * N, 16)) =
+        *reinterpret_cast<const uint4*>(w + j * N);
   if (DW) {
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
@@ -202,7 +221,7 @@ __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __re
       if (FULL || vi < nvec)
 #pragma unroll
         for (int q = 0; q < N / 4; ++q)
-          *reinterpret_cast<float4*>(acc + vi * N + 4 * q) = make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(acc + q * nvec * 4 + vi * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   __syncthreads();
@@ -231,7 +250,7 @@ __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __re
 #pragma unroll
       for (int q = 0; q < N / 4; ++q)
         *reinterpret_cast<float4*>(part + vi * N + 4 * q) =
-            *reinterpret_cast<const float4*>(acc + vi * N + 4 * q);
+            *reinterpret_cast<const float4*>(acc + q * nvec * 4 + vi * 4);
   }
 }
 

@@ -29,6 +29,7 @@ from ..parallel import state
 from ..parallel.buffers import divide, make_viewless_tensor
 from ..parallel import tensor as tp
 from ..ops.dropout import bias_dropout_add
+from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm
 from ..ops.rope import rope_table, apply_rope_ref
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func
@@ -390,6 +391,15 @@ class ParallelTransformerLayer(MegatronModule):
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None,
                 inference_params=None, position_ids=None):
+        if tracing():
+            with trace_range(f"layer{self.layer_number}"):
+                return self._forward(hidden_states, attention_mask, encoder_output,
+                                     enc_dec_attn_mask, inference_params, position_ids)
+        return self._forward(hidden_states, attention_mask, encoder_output, enc_dec_attn_mask,
+                             inference_params, position_ids)
+
+    def _forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None,
+                 inference_params=None, position_ids=None):
         if self._fused_residual_ok():
             return self._forward_fused_residual(hidden_states, attention_mask, inference_params,
                                                 position_ids)

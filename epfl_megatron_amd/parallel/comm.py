@@ -28,6 +28,8 @@ from collections import OrderedDict
 import torch
 import torch.distributed as dist
 
+from ..utils import trace as _trace
+
 _CHECK = os.environ.get("EMA_COMM_CHECK", "0") == "1"
 _TIMING = [False]
 _STATS = OrderedDict()  # key -> [count, bytes, ms]
@@ -140,7 +142,15 @@ class Work:
 
 def _issue(op, group, tensor_for_bytes, watch, fn, async_op):
     key = _key(op, group)
-    _account(key, tensor_for_bytes.numel() * tensor_for_bytes.element_size())
+    nbytes = tensor_for_bytes.numel() * tensor_for_bytes.element_size()
+    _account(key, nbytes)
+    if _trace.tracing():
+        with _trace.trace_range(f"comm:{key} {nbytes / 2**20:.1f}MiB"):
+            return _issue_inner(key, tensor_for_bytes, watch, fn, async_op)
+    return _issue_inner(key, tensor_for_bytes, watch, fn, async_op)
+
+
+def _issue_inner(key, tensor_for_bytes, watch, fn, async_op):
     start = None
     if _events_on(tensor_for_bytes):
         start = torch.cuda.Event(enable_timing=True)

@@ -22,6 +22,7 @@ from ..buffers import make_viewless_tensor
 from ... import global_vars
 from . import p2p
 from ...models.enums import ModelType
+from ...utils.trace import trace_range, tracing
 
 
 def get_forward_backward_func():
@@ -60,6 +61,16 @@ def _unwrap(model):
 
 def forward_step(forward_step_func, data_iterator, model, input_tensor, forward_data_store,
                  timers, collect_non_loss_data=False):
+    if tracing():
+        with trace_range("fwd-microbatch"):
+            return _forward_step(forward_step_func, data_iterator, model, input_tensor,
+                                 forward_data_store, timers, collect_non_loss_data)
+    return _forward_step(forward_step_func, data_iterator, model, input_tensor,
+                         forward_data_store, timers, collect_non_loss_data)
+
+
+def _forward_step(forward_step_func, data_iterator, model, input_tensor, forward_data_store,
+                  timers, collect_non_loss_data=False):
     if timers is not None:
         timers("forward-compute", log_level=2).start()
     unwrapped = _unwrap(model)
@@ -85,6 +96,14 @@ def forward_step(forward_step_func, data_iterator, model, input_tensor, forward_
 
 
 def backward_step(optimizer, input_tensor, output_tensor, output_tensor_grad, timers):
+    if tracing():
+        with trace_range("bwd-microbatch"):
+            return _backward_step(optimizer, input_tensor, output_tensor, output_tensor_grad,
+                                  timers)
+    return _backward_step(optimizer, input_tensor, output_tensor, output_tensor_grad, timers)
+
+
+def _backward_step(optimizer, input_tensor, output_tensor, output_tensor_grad, timers):
     if timers is not None:
         timers("backward-compute", log_level=2).start()
     unwrap_input = False

@@ -23,6 +23,7 @@ from .models.module import Float16Module
 from .optim import get_megatron_optimizer, OptimizerParamScheduler
 from .optim.optimizer import LazyScalar
 from .parallel import comm
+from .utils.trace import set_tracing, trace_range
 from .parallel import state
 from .parallel.ddp import DistributedDataParallel as LocalDDP
 from .parallel.pipeline.schedules import get_forward_backward_func
@@ -241,9 +242,11 @@ def train_step(forward_step_func, data_iterator, model, optimizer, opt_param_sch
     timers("forward-backward").stop()
     if args.empty_unused_memory_level >= 1 and torch.cuda.is_available():
         torch.cuda.empty_cache()
-    optimizer.reduce_model_grads(args, timers)
+    with trace_range("reduce-grads"):
+        optimizer.reduce_model_grads(args, timers)
     timers("optimizer", log_level=1).start(barrier=args.barrier_with_L1_time)
-    update_successful, grad_norm, num_zeros = optimizer.step(args, timers)
+    with trace_range("optimizer-step"):
+        update_successful, grad_norm, num_zeros = optimizer.step(args, timers)
     timers("optimizer").stop()
     # The skip decision is made on the device; the scheduler advances now and
     # is rolled back by the optimizer if the step turns out to be skipped.
@@ -399,6 +402,8 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
     total_loss_dict = {}
     iteration = args.iteration
     comm.set_timing(args.timing_log_level >= 2)
+    if args.timing_log_level >= 2:  # roctx / torch.profiler ranges (utils/trace.py)
+        set_tracing(True)
     timers("interval-time", log_level=0).start(barrier=True)
     print_datetime("before the start of training step")
     report_memory_flag = True

@@ -388,3 +388,20 @@ def test_bias_dropout_add_cpu_path():
     y = bias_dropout_add(x, b, r, 0.5, True, x2=x)
     kept = ((y - r).abs() > 1e-6).float().mean().item()
     assert 0.4 < kept < 0.6
+
+
+def test_trace_ranges_reach_torch_profiler():
+    """--timing_log_level 2 ranges (layers, micro-batches, collectives) are visible
+    to torch.profiler (and roctx on ROCm)."""
+    from epfl_megatron_amd.utils import trace
+    from epfl_megatron_amd.parallel import comm
+    trace.set_tracing(True)
+    try:
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+            with trace.trace_range("layer7"):
+                torch.ones(4).sum()
+        names = {e.name for e in prof.events()}
+        assert "layer7" in names
+    finally:
+        trace.set_tracing(False)
+    assert trace.trace_range("x") is trace.trace_range("y")  # shared no-op when off
