@@ -2,34 +2,33 @@
 //
 //     G[N, K] (+)= dY[M, N]^T · X[M, K]          dY, X bf16/fp16 row-major, G fp32
 //
-// This is the reference's fused_weight_gradient_dense (wgrad into main_grad,
-// SURVEY N8).  Both operands are "reduction-major" (the reduced token index m
-// is the slow dimension), the NT case that hipBLASLt serves at ~1000 TFLOP/s
-// on MI355X across all of its solutions (profiles/r1_lt_tune.json).
+// The reference's fused_weight_gradient_dense (wgrad into main_grad, SURVEY N8;
+// megatron/fused_kernels/fused_weight_gradient_dense.cu:129-152).  Both operands
+// are "reduction-major" (the reduced token index m is the slow dimension): the
+// NT case hipBLASLt serves at ~1.0 PF on MI355X whatever the solution
+// (profiles/r1_lt_tune.json), 2/3 of its TN rate.  On gfx950 the layout costs
+// nothing: ds_read_b64_tr_b16 turns a token-major LDS tile into MFMA operands.
 //
-// Design:
-//   * 256 x 256 output tile per workgroup, 8 waves (2 along N x 4 along K),
-//     each wave 128 x 64 = 4 x 2 tiles of v_mfma_f32_32x32x16 (128 fp32 acc).
-//   * Tokens are consumed in slots of BM = 32 rows.  Both operand slices
-//     [32 m][256] are staged HBM -> LDS with global_load_lds_dwordx4
-//     (lane-linear LDS image, XOR-swizzled through the per-lane SOURCE
-//     address) into a ring of 4 slots (4 x 32 KiB = 128 KiB LDS) with 3 slots
-//     in flight: the loads of slot t+3 are issued while slot t is consumed and
-//     completion is waited with a COUNTED vmcnt (never 0 in the steady state)
-//     plus a raw s_barrier — so ~1.3 us of HBM/L2 latency is hidden instead
-//     of the one-stage window of a 2-buffer loop (CDNA guide §5 "Pipelining
-//     across barriers").
-//   * MFMA operands come out of LDS with ds_read_b64_tr_b16 (inline asm, so
-//     the compiler cannot drain the LDS-DMA stream in front of them): a 16-lane
-//     group reads 4 token rows x 16 columns and receives it column-major —
-//     exactly the "8 consecutive k per lane" fragment both MFMA operands need.
-//     The swizzle chunk ^= (row & 3) << 2 makes every transposed read of a
-//     32-lane half hit 16 distinct 16-byte slots (conflict-free).  Fragment
-//     reads of k-step s+1 are issued before the MFMAs of k-step s (counted
-//     lgkmcnt).
-//   * Epilogue: batched read-modify-write of G in fp32 (beta = 1), or plain
-//     store (beta = 0, first micro-batch: main_grad is never zero-filled).
-//   * XCD-aware tile order: consecutive tiles of one XCD form 8 (N) x 4 (K)
+// Structure (the 256x256 ping-pong template of the CDNA guide §5, adapted):
+//   * 256 (n) x 256 (k) output tile per workgroup, 8 waves as 2 (n) x 4 (k),
+//     each wave 128 x 64 = 8 x 4 tiles of v_mfma_f32_16x16x32 (128 fp32 acc;
+//     16x16x32 holds a higher clock under load than 32x32x16, MICROARCH (7)).
+//   * Tokens are consumed in subtiles of 32 rows (one MFMA k-step).  Both
+//     operand slices [32 m][256] go HBM -> LDS by global_load_lds_dwordx4 into
+//     a ring of 4 subtiles (4 x 32 KiB); the loads of subtile p+3 are issued in
+//     phase p and retired by a COUNTED vmcnt, so ~3 phases (~1.3 us) of
+//     latency are hidden and no vmcnt(0) appears in the loop.
+//   * LDS image (a) of guide T10 ([32][256] as 8-row x 32-col 512-B subtiles,
+//     2-bit XOR inside each 64-B row piece), written lane-linearly by the DMA
+//     (the swizzle is applied through the per-lane SOURCE address).  Every
+//     transposed fragment read is conflict-free, and the fragments of a wave
+//     differ by instruction immediates: 4 base VGPRs per operand.
+//   * Ping-pong: waves 4..7 run one barrier behind waves 0..3 (two barriers
+//     per phase), so on every SIMD one wave's 32 MFMAs (s_setprio 1) overlap
+//     the other wave's fragment reads and DMA issue.
+//   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
+//     0: the first micro-batch of a step; main_grad is never zero-filled).
+//   * XCD-aware tile order: each XCD's consecutive tiles form 8 (n) x 4 (k)
 //     groups so concurrently running workgroups share operand panels in L2.
 //
 // Shapes: N % 256 == 0, K % 256 == 0, M % 32 == 0 (checked by the host).
@@ -38,64 +37,69 @@
 namespace ema {
 namespace {
 
-using fa::MT;
-using fa::f32x16;
+using fa::static_for;
 
-constexpr int TN = 256;                 // output rows (N) per tile
-constexpr int TK = 256;                 // output cols (K) per tile
-constexpr int BM = 32;                  // tokens per ring slot
-constexpr int ROWB = 512;               // bytes per LDS row (256 x 16-bit)
-constexpr int OPB = BM * ROWB;          // 16 KiB per operand slice
-constexpr int SLOTB = 2 * OPB;          // A + B
-constexpr int NSLOT = 4;                // ring depth (NSLOT - 1 slots in flight)
-constexpr int LDSB = NSLOT * SLOTB;     // 128 KiB
-constexpr int LOADS = 4;                // glds instructions per wave per slot
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row & 3) << 2); }
+constexpr int TN = 256;               // output rows (n) per tile
+constexpr int TK = 256;               // output cols (k) per tile
+constexpr int BM = 32;                // tokens per subtile = one MFMA k-step
+constexpr int OPB = BM * TN * 2;      // 16 KiB per operand subtile
+constexpr int SLOTB = 2 * OPB;        // dY + X
+constexpr int NSLOT = 4;              // ring depth (3 subtiles ahead)
+constexpr int LDSB = NSLOT * SLOTB;   // 128 KiB
+constexpr int LOADS = 4;              // glds instructions per wave per subtile
+constexpr int FA_ = 8, FB_ = 4;       // A (n) and B (k) fragments per wave
 
-// Stage one [32][256] slice of a row-major [M][ld] matrix (cols c0..c0+255,
-// rows m0..m0+31) at LDS byte offset `dst`: 8 waves x 2 instructions, each
-// instruction = 2 rows x 512 B, lane-linear in LDS.
+// Image (a): byte offset of 16-B chunk `ch` (0..31) of row `row` (0..31).
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return 4096 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// Stage the [32 m][256] slice of a row-major [M][ld] matrix (cols c0..c0+255,
+// rows m0..m0+31) at LDS byte offset `dst`: 16 pieces of 1 KiB, 2 per wave.
 template <typename T>
 __device__ __forceinline__ void stage_op(const T* __restrict__ src, int64_t ld, int64_t m0,
                                          int64_t c0, char* lds, int dst, int wave, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int inst = wave * 2 + i;
-    const int row = 2 * inst + (lane >> 5);
-    const int chunk = swz_chunk(row, lane & 31);  // involution: source chunk for this lane
-    const T* g = src + (m0 + row) * ld + c0 + chunk * 8;
+    const int piece = wave * 2 + i;
+    const int o = piece * 1024 + lane * 16;  // LDS byte this lane's 16 B land on
+    const int rem = o & 4095;
+    const int row = 8 * (o >> 12) + ((rem >> 6) & 7);
+    const int ch = 4 * (rem >> 9) + (((rem >> 4) & 3) ^ ((row >> 2) & 3));
+    const T* g = src + (m0 + row) * ld + c0 + ch * 8;
     __builtin_amdgcn_global_load_lds(
-        (const void*)g, (__attribute__((address_space(3))) void*)(lds + dst + inst * 1024), 16, 0,
+        (const void*)g, (__attribute__((address_space(3))) void*)(lds + dst + piece * 1024), 16, 0,
         0);
   }
 }
 
-// ds_read_b64_tr_b16 as inline asm: invisible to the compiler's LDS-DMA alias
-// tracking, so no vmcnt(0) is inserted in front of it.
-__device__ __forceinline__ fa::bf16x4 tr_read_asm(uint32_t addr) {
-  fa::bf16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
+// Lane's transposed-read address for the 16-column fragment whose first
+// column has (c0 / 16) parity `par` inside a 32-column group, token rows
+// 8g + 4u + q (g = lane >> 4): the fragment at column cb + 16 f reads at
+// base(par = f & 1, u) + 512 * (f >> 1) (+ the 32-col group of cb).
+__device__ __forceinline__ uint32_t frag_base(int cb, int par, int u, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int row = 8 * g + 4 * u + q;
+  const int ch = (cb >> 3) + 2 * par + (p >> 1);
+  return (uint32_t)(img_off(row, ch) + 8 * (p & 1));
 }
 
-// Byte address (within a slice) of this lane's transposed read of token rows
-// r0+q (q = 0..3 from the lane) for columns c0 + 16*g + 4*p.
-__device__ __forceinline__ uint32_t tr_addr(int r0, int c0, int lane) {
-  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
-  const int col = c0 + ((lane >> 4) & 1) * 16 + 4 * p;
-  const int r = r0 + q;
-  return (uint32_t)(r * ROWB + swz_chunk(r, col >> 3) * 16 + ((col >> 2) & 1) * 8);
-}
-
-// Wait until at most `slots` slots' LDS-DMA loads of this wave are in flight
-// (wave-uniform argument; vmcnt needs an immediate).
-__device__ __forceinline__ void wait_slots(int slots) {
-  static_assert(LOADS == 4, "vmcnt immediates below assume 4 loads per slot");
-  if (slots >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (slots == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (slots == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+// Wait until at most `n` subtiles' DMA of this wave are outstanding
+// (wave-uniform; vmcnt takes an immediate).
+__device__ __forceinline__ void wait_subtiles(int n) {
+  static_assert(LOADS == 4, "vmcnt immediates assume 4 glds per subtile");
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::MT<T>::x8 b,
+                                        f32x4 c) {
+  if constexpr (__is_same(T, bf16)) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
 template <typename T, bool ACCUM, int MODE = 0>
@@ -104,11 +108,10 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
         int K) {
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wn = wave >> 2, wk = wave & 3;
-  const int h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave >> 2, wk = wave & 3;  // wn is also the ping-pong group
 
-  // tile order: XCD-contiguous, then 8 (N) x 4 (K) groups
+  // tile order: XCD-contiguous, then 8 (n) x 4 (k) groups
   const int ntn = N / TN, ntk = K / TK, ntiles = ntn * ntk;
   const int lin = xcd_remap(blockIdx.x, ntiles);
   constexpr int GN = 8;
@@ -120,54 +123,63 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   const int tk = in_grp / gsize;
   const int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
 
-  f32x16 acc[4][2];
+  f32x4 acc[FA_][FB_];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FA_; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int j = 0; j < FB_; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint32_t a_off[4], b_off[2];
+  // 4 bases per operand: [parity][u]; B lives OPB after A in a slot
+  uint32_t abase[2][2], bbase[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) a_off[i] = tr_addr(8 * h, wn * 128 + 32 * i, lane);
+  for (int par = 0; par < 2; ++par)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) b_off[j] = tr_addr(8 * h, wk * 64 + 32 * j, lane);
+    for (int u = 0; u < 2; ++u) {
+      abase[par][u] = frag_base(wn * 128, par, u, lane);
+      bbase[par][u] = OPB + frag_base(wk * 64, par, u, lane);
+    }
   const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
 
   auto stage = [&](int t) {  // slot t % NSLOT <- tokens [t*BM, t*BM + BM)
-    if constexpr (MODE == 2) return;  // experiment: no HBM/L2 traffic in the main loop
+    if constexpr (MODE == 2) return;  // ablation: no HBM/L2 traffic in the main loop
     const int dst = (t % NSLOT) * SLOTB;
     stage_op<T>(dy, N, (int64_t)t * BM, n0, lds, dst, wave, lane);
     stage_op<T>(x, K, (int64_t)t * BM, k0, lds, dst + OPB, wave, lane);
   };
 
-  // Fragment registers: two sets, always one k-step (16 tokens) ahead.
-  fa::bf16x4 fa_[2][4][2], fb_[2][2][2];
-  auto issue = [&](int t, int s, int set) {  // k-step s (0/1) of slot t
-    const uint32_t ca = lds_base + (t % NSLOT) * SLOTB + (16 * s) * ROWB, cb = ca + OPB;
+  typename fa::MT<T>::x4 fa_[FA_][2], fb_[FB_][2];
+  auto reads = [&](int t) {  // all fragments of subtile t (24 transposed reads)
+    const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
+    uint32_t a[2][2], b[2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int par = 0; par < 2; ++par)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) fa_[set][i][u] = tr_read_asm(ca + a_off[i] + 4 * u * ROWB);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) fb_[set][j][u] = tr_read_asm(cb + b_off[j] + 4 * u * ROWB);
+      for (int u = 0; u < 2; ++u) {
+        a[par][u] = so + abase[par][u];
+        b[par][u] = so + bbase[par][u];
+      }
+    static_for<FA_>([&](auto f) {
+      constexpr int F = decltype(f)::value;
+      fa_[F][0] = fa::tr_read_imm<512 * (F >> 1), T>(a[F & 1][0]);
+      fa_[F][1] = fa::tr_read_imm<512 * (F >> 1), T>(a[F & 1][1]);
+    });
+    static_for<FB_>([&](auto f) {
+      constexpr int F = decltype(f)::value;
+      fb_[F][0] = fa::tr_read_imm<512 * (F >> 1), T>(b[F & 1][0]);
+      fb_[F][1] = fa::tr_read_imm<512 * (F >> 1), T>(b[F & 1][1]);
+    });
   };
-  auto mfmas = [&](int set) {
-    typename MT<T>::x8 a[4], b[2];
+  auto mfmas = [&]() {
+    typename fa::MT<T>::x8 av[FA_], bv[FB_];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      a[i] = __builtin_bit_cast(typename MT<T>::x8, fa::join<bf16>(fa_[set][i][0], fa_[set][i][1]));
+    for (int i = 0; i < FA_; ++i) av[i] = fa::join<T>(fa_[i][0], fa_[i][1]);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      b[j] = __builtin_bit_cast(typename MT<T>::x8, fa::join<bf16>(fb_[set][j][0], fb_[set][j][1]));
+    for (int j = 0; j < FB_; ++j) bv[j] = fa::join<T>(fb_[j][0], fb_[j][1]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FA_; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = MT<T>::mfma(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < FB_; ++j) acc[i][j] = mfma16<T>(av[i], bv[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -175,67 +187,66 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
 #pragma unroll
   for (int t = 0; t < NSLOT - 1; ++t)
     if (t < nt) stage(t);
-  wait_slots(min(nt, NSLOT - 1) - 1);  // slot 0 landed, the rest may be in flight
-  __builtin_amdgcn_s_barrier();
-  issue(0, 0, 0);
+  wait_subtiles(min(nt, NSLOT - 1) - 1);  // subtile 0 landed (own DMA)
+  __builtin_amdgcn_s_barrier();            // ... and everyone's
+  if (wn == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
 
-  // Per slot t:   [reads (t,1)] [MFMA (t,0)] [wait slot t+1, barrier, stage t+3]
-  //               [reads (t+1,0)] [MFMA (t,1)]
-  // The barrier sits mid-slot, so the MFMAs of (t,0) cover it and the
-  // fragment reads never drain across a slot boundary.  RAW: slot t+1's
-  // loads are waited (counted vmcnt) by every wave before the barrier.  WAR:
-  // slot t+3 reuses slot t-1, whose reads all completed before the MFMAs of
-  // (t-1,1), i.e. before this barrier in every wave.
+  // Phase p: [reads p][stage p+3][vmcnt: p+1 landed][lgkmcnt(0)] BAR_A
+  //          [32 MFMA] BAR_B
+  // Group 0's BAR_A(p) is barrier 2p+1, group 1's is 2p+2 (= group 0's
+  // BAR_B(p)): each group's MFMA section overlaps the other's load section.
+  // RAW: subtile p+1 is retired by every wave before its BAR_A(p); both
+  //      groups read it only after a later barrier.
+  // WAR: stage(p+3) overwrites subtile p-1, whose reads every wave retired
+  //      (lgkmcnt(0)) before its BAR_A(p-1), a barrier both groups passed.
   for (int t = 0; t < nt; ++t) {
-    issue(t, 1, 1);
-    asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+    reads(t);
+    if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
+    wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    mfmas(0);
-    if (t + 1 < nt) {
-      // slots issued after t+1 may stay in flight: t+2 .. min(t+NSLOT-2, nt-1)
-      wait_slots(min(t + NSLOT - 2, nt - 1) - (t + 1));
-      __builtin_amdgcn_s_barrier();
-      if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
-      issue(t + 1, 0, 0);
-      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    __builtin_amdgcn_s_barrier();
+    mfmas();
     __builtin_amdgcn_sched_barrier(0);
-    mfmas(1);
+    __builtin_amdgcn_s_barrier();
   }
+  if (wn == 0) __builtin_amdgcn_s_barrier();  // balance the barrier count
 
-  // epilogue: G[n][k] (+)= acc ; col = lane & 31, row = acc_row(reg, h)
-  if constexpr (MODE == 1) {  // experiment: keep acc alive, skip the epilogue traffic
+  // epilogue: G[n][k] (+)= acc; lane holds col lane&15, rows 4(lane>>4) + r
+  if constexpr (MODE == 1) {  // ablation: keep acc alive, skip the epilogue traffic
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FA_; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) s += acc[i][j][0] + acc[i][j][15];
+      for (int j = 0; j < FB_; ++j) s += acc[i][j][0] + acc[i][j][3];
     if (s == 1234567.f) g[threadIdx.x] = s;
     return;
   }
+  const int64_t col = k0 + wk * 64 + (lane & 15);
+  const int64_t row0 = n0 + wn * 128 + 4 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FA_; ++i) {
+    float* base = g + (row0 + 16 * i) * (int64_t)K + col;
+    if (ACCUM) {  // batch the 16 loads, then one wait, then the stores
+      float old[FB_][4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = k0 + wk * 64 + 32 * j + (lane & 31);
-      float* base = g + (n0 + wn * 128 + 32 * i) * (int64_t)K + col;
-      if (ACCUM) {  // batch the 16 loads, then one wait, then the stores
-        float old[16];
+      for (int j = 0; j < FB_; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          old[r] = __builtin_nontemporal_load(base + (int64_t)fa::acc_row(r, h) * K);
+        for (int r = 0; r < 4; ++r)
+          old[j][r] = __builtin_nontemporal_load(base + (int64_t)r * K + 16 * j);
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_nontemporal_store(old[r] + acc[i][j][r],
-                                      base + (int64_t)fa::acc_row(r, h) * K);
-      } else {
+      for (int j = 0; j < FB_; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_nontemporal_store(acc[i][j][r], base + (int64_t)fa::acc_row(r, h) * K);
-      }
+        for (int r = 0; r < 4; ++r)
+          __builtin_nontemporal_store(old[j][r] + acc[i][j][r], base + (int64_t)r * K + 16 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < FB_; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __builtin_nontemporal_store(acc[i][j][r], base + (int64_t)r * K + 16 * j);
     }
+  }
 }
 
 template <typename T, bool ACCUM, int MODE = 0>

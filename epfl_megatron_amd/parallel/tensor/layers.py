@@ -162,7 +162,7 @@ def _notify_grad_ready(param):
 # kernel; the default stays hipBLASLt while it measures faster in the full
 # 7B step (profiles/r1_wgrad_ab.txt: 22.90k vs 22.24k tokens/s on 1 MI355X,
 # the kernel reaching ~1000 TFLOP/s like hipBLASLt in isolation).
-_WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hipblaslt").lower() == "hip"
+_WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hip").lower() == "hip"
 # EMA_GEMM=tuned routes all three products through ops/gemm.py (per-shape
 # solution timing).  Off by default: in the full 7B step it measured 22.4k vs
 # 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —

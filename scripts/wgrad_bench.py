@@ -44,7 +44,7 @@ def check():
 def main():
     check()
     C = ext()
-    M = 8192
+    M = 16384  # tokens of one 7B micro-batch (16 x 1024)
     out = {}
     for name, (N, K) in SHAPES.items():
         dY = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
@@ -68,7 +68,7 @@ def main():
 def ablation():
     """Time the ablation builds on fc1 (mode 1: no epilogue, 2: no global loads)."""
     C = ext()
-    M, N, K = 8192, 22016, 4096
+    M, N, K = 16384, 22016, 4096
     dY = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) - 0.5
     X = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) - 0.5
     G = torch.zeros(N, K, device="cuda", dtype=torch.float32)
