@@ -25,7 +25,11 @@
 //     differ by instruction immediates: 4 base VGPRs per operand.
 //   * Ping-pong: waves 4..7 run one barrier behind waves 0..3 (two barriers
 //     per phase), so on every SIMD one wave's 32 MFMAs (s_setprio 1) overlap
-//     the other wave's fragment reads and DMA issue.
+//     the other wave's fragment reads.  The DMA of subtile p+3 is issued from
+//     inside the MFMA section (SCHED 2, the production schedule): in the load
+//     section its ~60-cycle issue cost made that section the critical path
+//     (fc1 shape: 1.25 vs 1.09-1.16 PF; SCHED 1, a non-ping-pong schedule
+//     with the reads interleaved between the MFMAs, 1.06-1.08 PF).
 //   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
 //     0: the first micro-batch of a step; main_grad is never zero-filled).
 //   * XCD-aware tile order: each XCD's consecutive tiles form 8 (n) x 4 (k)
@@ -102,7 +106,7 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
   else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-template <typename T, bool ACCUM, int MODE = 0>
+template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
         int K) {
@@ -147,6 +151,8 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     stage_op<T>(x, K, (int64_t)t * BM, k0, lds, dst + OPB, wave, lane);
   };
 
+  const int nt = M / BM;
+  if constexpr (SCHED != 1) {
   typename fa::MT<T>::x4 fa_[FA_][2], fb_[FB_][2];
   auto reads = [&](int t) {  // all fragments of subtile t (24 transposed reads)
     const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
@@ -169,21 +175,33 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       fb_[F][1] = fa::tr_read_imm<512 * (F >> 1), T>(b[F & 1][1]);
     });
   };
-  auto mfmas = [&]() {
+  auto mfmas = [&](int t) {
     typename fa::MT<T>::x8 av[FA_], bv[FB_];
 #pragma unroll
     for (int i = 0; i < FA_; ++i) av[i] = fa::join<T>(fa_[i][0], fa_[i][1]);
 #pragma unroll
     for (int j = 0; j < FB_; ++j) bv[j] = fa::join<T>(fb_[j][0], fb_[j][1]);
     __builtin_amdgcn_s_setprio(1);
+    static_for<FA_>([&](auto i) {
+      constexpr int I = decltype(i)::value;
 #pragma unroll
-    for (int i = 0; i < FA_; ++i)
-#pragma unroll
-      for (int j = 0; j < FB_; ++j) acc[i][j] = mfma16<T>(av[i], bv[j], acc[i][j]);
+      for (int j = 0; j < FB_; ++j) acc[I][j] = mfma16<T>(av[I], bv[j], acc[I][j]);
+      // SCHED 2: the DMA of subtile t+3 rides in the MFMA section (rows 1, 5)
+      if constexpr (SCHED == 2 && MODE != 2 && (I == 1 || I == 5)) {
+        const int ts = t + NSLOT - 1;
+        if (ts < nt) {
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (I == 1)
+            stage_op<T>(dy, N, (int64_t)ts * BM, n0, lds, (ts % NSLOT) * SLOTB, wave, lane);
+          else
+            stage_op<T>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    });
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nt = M / BM;
 #pragma unroll
   for (int t = 0; t < NSLOT - 1; ++t)
     if (t < nt) stage(t);
@@ -199,18 +217,91 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   //      groups read it only after a later barrier.
   // WAR: stage(p+3) overwrites subtile p-1, whose reads every wave retired
   //      (lgkmcnt(0)) before its BAR_A(p-1), a barrier both groups passed.
+  // SCHED 2 issues stage(p+3) after BAR_A(p) instead (still after the
+  // retirement of subtile p-1's reads), so one subtile fewer is in flight at
+  // the vmcnt of the load section.
   for (int t = 0; t < nt; ++t) {
     reads(t);
-    if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
-    wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
+    if constexpr (SCHED == 0) {
+      if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
+      wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
+    } else {
+      wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    mfmas();
+    mfmas(t);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
   if (wn == 0) __builtin_amdgcn_s_barrier();  // balance the barrier count
+
+  } else {
+    // SCHED 1: no ping-pong, one barrier per phase.  Phase p runs the 32
+    // MFMAs of subtile p (fragments read during phase p-1) interleaved with
+    // the 24 transposed reads of subtile p+1 and the DMA of subtile p+3.
+    // RAW: subtile p+1 is retired (counted vmcnt) by every wave before the
+    //      barrier that ends phase p-1.
+    // WAR: stage(p+3) overwrites subtile p-1, read during phase p-2 and
+    //      retired (lgkmcnt(0)) before the barrier ending phase p-2.
+    typename fa::MT<T>::x4 fr[2][FA_ + FB_][2];
+    auto rd = [&](auto set, int t, auto f) {  // fragment f (A: 0..7, B: 8..11) of subtile t
+      constexpr int S = decltype(set)::value, F = decltype(f)::value;
+      const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
+      if constexpr (F < FA_) {
+        fr[S][F][0] = fa::tr_read_imm<512 * (F >> 1), T>(so + abase[F & 1][0]);
+        fr[S][F][1] = fa::tr_read_imm<512 * (F >> 1), T>(so + abase[F & 1][1]);
+      } else {
+        constexpr int G = F - FA_;
+        fr[S][F][0] = fa::tr_read_imm<512 * (G >> 1), T>(so + bbase[G & 1][0]);
+        fr[S][F][1] = fa::tr_read_imm<512 * (G >> 1), T>(so + bbase[G & 1][1]);
+      }
+    };
+    auto phase = [&](auto cur, int t) {
+      constexpr int C = decltype(cur)::value, NX = 1 - C;
+      const bool more = t + 1 < nt, stg = t + NSLOT - 1 < nt;
+      typename fa::MT<T>::x8 bv[FB_];
+      static_for<FB_>([&](auto j) { bv[j] = fa::join<T>(fr[C][FA_ + j][0], fr[C][FA_ + j][1]); });
+      static_for<FA_>([&](auto i) {
+        constexpr int I = decltype(i)::value;
+        const typename fa::MT<T>::x8 av = fa::join<T>(fr[C][I][0], fr[C][I][1]);
+        __builtin_amdgcn_sched_barrier(0);
+        // the next subtile's 12 fragments over the 8 MFMA rows: row I reads
+        // A fragment I, rows 0-3 also B fragment I; rows 1 and 5 issue the DMA
+        if (more) {
+          rd(std::integral_constant<int, NX>{}, t + 1, std::integral_constant<int, I>{});
+          if constexpr (I < FB_) rd(std::integral_constant<int, NX>{}, t + 1,
+                                    std::integral_constant<int, FA_ + I>{});
+        }
+        if constexpr (I == 1 && MODE != 2) { if (stg) stage_op<T>(dy, N, (int64_t)(t + NSLOT - 1) * BM, n0, lds,
+                                                     ((t + NSLOT - 1) % NSLOT) * SLOTB, wave, lane); }
+        if constexpr (I == 5 && MODE != 2) { if (stg) stage_op<T>(x, K, (int64_t)(t + NSLOT - 1) * BM, k0, lds,
+                                                     ((t + NSLOT - 1) % NSLOT) * SLOTB + OPB, wave, lane); }
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<FB_>([&](auto j) { acc[I][j] = mfma16<T>(av, bv[j], acc[I][j]); });
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 2));  // subtile t+2 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll
+    for (int t = 0; t < NSLOT - 1; ++t)
+      if (t < nt) stage(t);
+    wait_subtiles(min(nt, NSLOT - 1) - 2);  // subtiles 0 and 1 landed (own DMA)
+    __builtin_amdgcn_s_barrier();
+    static_for<FA_ + FB_>([&](auto f) { rd(std::integral_constant<int, 0>{}, 0, f); });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+      phase(std::integral_constant<int, 0>{}, t);
+      phase(std::integral_constant<int, 1>{}, t + 1);
+    }
+    if (t < nt) phase(std::integral_constant<int, 0>{}, t);
+  }
 
   // epilogue: G[n][k] (+)= acc; lane holds col lane&15, rows 4(lane>>4) + r
   if constexpr (MODE == 1) {  // ablation: keep acc alive, skip the epilogue traffic
@@ -249,22 +340,34 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   }
 }
 
-template <typename T, bool ACCUM, int MODE = 0>
+template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s) {
   const int ntiles = (N / TN) * (K / TK);
-  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE>), dim3(ntiles), dim3(512), 0, s, (const T*)dy,
-                     (const T*)x, g, M, N, K);
+  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(ntiles), dim3(512), 0, s,
+                     (const T*)dy, (const T*)x, g, M, N, K);
 }
 
 }  // namespace
 
-// Ablation builds for profiling (bf16, accumulate): 1 = no epilogue traffic,
-// 2 = no global loads in the main loop (LDS/MFMA/barrier pipeline only).
+// Ablation builds for profiling (bf16, accumulate): mode % 10 = 1 no epilogue
+// traffic, 2 no global loads in the main loop; mode / 10 = schedule variant.
 void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
                          int64_t K, int mode, hipStream_t s) {
-  if (mode == 1) launch<bf16, true, 1>(dy, x, g, (int)M, (int)N, (int)K, s);
-  else if (mode == 2) launch<bf16, true, 2>(dy, x, g, (int)M, (int)N, (int)K, s);
-  else launch<bf16, true, 0>(dy, x, g, (int)M, (int)N, (int)K, s);
+  const int m = mode % 10, v = mode / 10;
+  const int iM = (int)M, iN = (int)N, iK = (int)K;
+  if (v == 2) {
+    if (m == 1) launch<bf16, true, 1, 2>(dy, x, g, iM, iN, iK, s);
+    else if (m == 2) launch<bf16, true, 2, 2>(dy, x, g, iM, iN, iK, s);
+    else launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 1) {
+    if (m == 1) launch<bf16, true, 1, 1>(dy, x, g, iM, iN, iK, s);
+    else if (m == 2) launch<bf16, true, 2, 1>(dy, x, g, iM, iN, iK, s);
+    else launch<bf16, true, 0, 1>(dy, x, g, iM, iN, iK, s);
+  } else {
+    if (m == 1) launch<bf16, true, 1, 0>(dy, x, g, iM, iN, iK, s);
+    else if (m == 2) launch<bf16, true, 2, 0>(dy, x, g, iM, iN, iK, s);
+    else launch<bf16, true, 0, 0>(dy, x, g, iM, iN, iK, s);
+  }
 }
 
 bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
@@ -275,12 +378,13 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
 
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
                 bool accumulate, int dt, hipStream_t s) {
+  const int iM = (int)M, iN = (int)N, iK = (int)K;
   if (dt == DT_BF16) {
-    if (accumulate) launch<bf16, true>(dy, x, g, (int)M, (int)N, (int)K, s);
-    else launch<bf16, false>(dy, x, g, (int)M, (int)N, (int)K, s);
+    if (accumulate) launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
+    else launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s);
   } else if (dt == DT_F16) {
-    if (accumulate) launch<fp16, true>(dy, x, g, (int)M, (int)N, (int)K, s);
-    else launch<fp16, false>(dy, x, g, (int)M, (int)N, (int)K, s);
+    if (accumulate) launch<fp16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
+    else launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s);
   }
 }
 
