@@ -31,7 +31,9 @@
 //     (fc1 shape: 1.25 vs 1.09-1.16 PF; SCHED 1, a non-ping-pong schedule
 //     with the reads interleaved between the MFMAs, 1.06-1.08 PF).
 //   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
-//     0: the first micro-batch of a step; main_grad is never zero-filled).
+//     0: the first micro-batch of a step; main_grad is never zero-filled),
+//     transposed through LDS so G moves in 16-B row pieces (+1.5 % on fc1
+//     over per-lane 4-B accesses).
 //   * XCD-aware tile order: each XCD's consecutive tiles form 8 (n) x 4 (k)
 //     groups so concurrently running workgroups share operand panels in L2.
 //
@@ -313,30 +315,48 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     if (s == 1234567.f) g[threadIdx.x] = s;
     return;
   }
-  const int64_t col = k0 + wk * 64 + (lane & 15);
-  const int64_t row0 = n0 + wn * 128 + 4 * (lane >> 4);
+  // Through LDS (free now: every ring read was retired before the last
+  // barrier, no DMA is in flight): each wave transposes its 128 x 64 fp32
+  // tile in two 64-row halves through a private 16 KiB region, so G moves
+  // as 16-B row pieces (256 B contiguous per 16 lanes) instead of 4-B
+  // pieces (64 B per 16 lanes).  Region layout: row-major [64][64] fp32
+  // with the 16-column group XOR-ed by (row >> 2) & 3 (conflict-free
+  // ds_write_b32 of the accumulator layout and ds_read_b128 of rows).
+  float* reg = reinterpret_cast<float*>(lds) + wave * 4096;
+  const int gq = lane >> 4, cl = lane & 15;
 #pragma unroll
-  for (int i = 0; i < FA_; ++i) {
-    float* base = g + (row0 + 16 * i) * (int64_t)K + col;
-    if (ACCUM) {  // batch the 16 loads, then one wait, then the stores
-      float old[FB_][4];
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < FB_; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          old[j][r] = __builtin_nontemporal_load(base + (int64_t)r * K + 16 * j);
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * i + 4 * gq + r;  // (lr >> 2) & 3 == gq
+          reg[lr * 64 + ((16 * j) ^ (16 * gq)) + cl] = acc[4 * h + i][j][r];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f32x4 v[16];
 #pragma unroll
-      for (int j = 0; j < FB_; ++j)
+    for (int k = 0; k < 16; ++k) {
+      const int lr = gq + 4 * k, c = 4 * cl;
+      v[k] = *reinterpret_cast<const f32x4*>(reg + lr * 64 + (c ^ (16 * ((lr >> 2) & 3))));
+    }
+    float* gb = g + (n0 + wn * 128 + 64 * h + gq) * (int64_t)K + k0 + wk * 64 + 4 * cl;
+    if (ACCUM) {
+      f32x4 o[16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          __builtin_nontemporal_store(old[j][r] + acc[i][j][r], base + (int64_t)r * K + 16 * j);
+      for (int k = 0; k < 16; ++k)
+        o[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(gb + (int64_t)(4 * k) * K));
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        __builtin_nontemporal_store(o[k] + v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * K));
     } else {
 #pragma unroll
-      for (int j = 0; j < FB_; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          __builtin_nontemporal_store(acc[i][j][r], base + (int64_t)r * K + 16 * j);
+      for (int k = 0; k < 16; ++k)
+        __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * K));
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before reuse
   }
 }
 
