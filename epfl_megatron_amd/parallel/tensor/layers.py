@@ -7,9 +7,9 @@ not split.
 
 MI355X-specific design of the GEMM path (``_LinearFn``):
 
-* Forward, dgrad and wgrad GEMMs run on hipBLASLt through PyTorch
-  (``EMA_GEMM=tuned`` switches to ``ops/gemm.py``'s per-shape solution
-  timing; ``EMA_WGRAD=hip`` to the hand-written MFMA wgrad kernel).
+* Forward and dgrad GEMMs run on hipBLASLt through PyTorch (``EMA_GEMM=tuned``
+  switches to ``ops/gemm.py``'s per-shape solution timing); the wgrad GEMM
+  on the hand-written MFMA kernel (``EMA_WGRAD=hipblaslt`` for the library).
 * With ``gradient_accumulation_fusion`` the weight gradient is a
   bf16 x bf16 -> fp32 GEMM written **in place** into the fp32 ``main_grad``
   view of the DDP bucket —
@@ -158,11 +158,13 @@ def _notify_grad_ready(param):
         cb()
 
 
-# Weight-gradient GEMM backend.  EMA_WGRAD=hip selects the hand-written MFMA
-# kernel; the default stays hipBLASLt while it measures faster in the full
-# 7B step (profiles/r1_wgrad_ab.txt: 22.90k vs 22.24k tokens/s on 1 MI355X,
-# the kernel reaching ~1000 TFLOP/s like hipBLASLt in isolation).
+# Weight-gradient GEMM backend: the hand-written MFMA kernel (csrc/gemm_wgrad.hip,
+# default; EMA_WGRAD=hipblaslt for the library): 1.11-1.40 PF isolated vs
+# 0.94-1.16 PF and 28.3k vs 26.7k tokens/s in the 7B step (profiles/r2_wgrad_ab.txt).
 _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hip").lower() == "hip"
+# One 256x256 output tile per workgroup and no split over tokens: below one
+# tile per CU (TP-sharded 7B/70B projections) hipBLASLt's split-K wins.
+_WGRAD_MIN_TILES = 256
 # EMA_GEMM=tuned routes all three products through ops/gemm.py (per-shape
 # solution timing).  Off by default: in the full 7B step it measured 22.4k vs
 # 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —
@@ -224,7 +226,8 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
     instead of zero-filling the buffer) makes the first contribution of a step
     a plain store (beta = 0): no fill kernel, no read of the old values.  On
     the GPU the hand-written MFMA kernel (``csrc/gemm_wgrad.hip``) is used for
-    every shape it tiles; others go to hipBLASLt through ``torch.addmm``.
+    every shape it tiles with at least one tile per CU; others go to
+    hipBLASLt through ``torch.addmm``.
     """
     main_grad = weight.main_grad
     accumulate = not getattr(weight, "_mg_fresh", False)
@@ -233,7 +236,8 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
         M, N = grad_output_2d.shape
         K = input_2d.shape[1]
         if _WGRAD_KERNEL and main_grad.is_contiguous() and grad_output_2d.is_contiguous() \
-                and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K):
+                and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K) \
+                and (N // 256) * (K // 256) >= _WGRAD_MIN_TILES:
             ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
         elif _TUNED_GEMM:
             tuned_gemm.wgrad(main_grad.view(N, K), grad_output_2d, input_2d, accumulate)
