@@ -43,6 +43,32 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
     return args
 
 
+def rccl_watchdog_env(timeout_minutes, environ=None):
+    """RCCL hang / failure detection (the reference relies on the
+    bare process-group timeout, ``megatron/initialize.py:150``).
+
+    * ``TORCH_NCCL_ASYNC_ERROR_HANDLING=3``: a collective that errors or
+      exceeds the process-group timeout tears the process down instead of
+      blocking forever, so torchrun / the scheduler sees a dead rank;
+    * ``TORCH_NCCL_ENABLE_MONITORING=1`` with a heartbeat timeout of the same
+      length: the watchdog thread itself is watched, and a wedged watchdog
+      also aborts (with a stack dump);
+    * ``TORCH_NCCL_DUMP_ON_TIMEOUT=1``: the flight recorder of the last
+      collectives is dumped when that happens.
+    Values already in the environment win.  Returns the settings applied."""
+    environ = os.environ if environ is None else environ
+    want = {
+        "TORCH_NCCL_ASYNC_ERROR_HANDLING": "3",
+        "TORCH_NCCL_ENABLE_MONITORING": "1",
+        "TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC": str(max(60, int(timeout_minutes * 60))),
+        "TORCH_NCCL_DUMP_ON_TIMEOUT": "1",
+        "TORCH_NCCL_TRACE_BUFFER_SIZE": "2000",
+    }
+    for k, v in want.items():
+        environ.setdefault(k, v)
+    return {k: environ[k] for k in want}
+
+
 def _initialize_distributed(args):
     use_gpu = torch.cuda.is_available()
     if use_gpu:
@@ -61,6 +87,7 @@ def _initialize_distributed(args):
         kw = {}
         if use_gpu and backend == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            rccl_watchdog_env(args.distributed_timeout_minutes)
         dist.init_process_group(backend=backend, world_size=args.world_size, rank=args.rank,
                                 timeout=datetime.timedelta(minutes=args.distributed_timeout_minutes),
                                 **kw)

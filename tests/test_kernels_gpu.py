@@ -542,3 +542,34 @@ def test_bias_dropout_add_autograd_and_rng_stream():
     with tracker.fork():
         y3 = bias_dropout_add(x, bias, r, 0.25, True)
     assert not torch.equal(y3, y1)
+
+
+def test_deterministic_attention_backward_and_wgrad():
+    """Deterministic mode by construction: the FA backward has no
+    atomics (dK/dV summed over a GQA group inside one workgroup, dQ by the
+    query-owning workgroup) and the wgrad GEMM reduces each tile in one
+    workgroup, so repeated runs are bitwise identical."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func
+    torch.manual_seed(5)
+    q = torch.randn(2, 512, 8, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(2, 512, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(2, 512, 2, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(2, 512, 8, 128, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        q.grad = k.grad = v.grad = None
+        flash_attn_func(q, k, v, causal=True).backward(g)
+        outs.append((q.grad.clone(), k.grad.clone(), v.grad.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+    C = _ext()
+    dy = torch.randn(4096, 512, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(4096, 768, device=DEV, dtype=torch.bfloat16)
+    g0 = torch.randn(512, 768, device=DEV)
+    res = []
+    for _ in range(3):
+        gg = g0.clone()
+        C.wgrad_gemm(dy, x, gg, True)
+        res.append(gg)
+    assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])

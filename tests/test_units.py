@@ -405,3 +405,14 @@ def test_trace_ranges_reach_torch_profiler():
     finally:
         trace.set_tracing(False)
     assert trace.trace_range("x") is trace.trace_range("y")  # shared no-op when off
+
+
+def test_rccl_watchdog_env():
+    """RCCL watchdog settings: set when absent, never override the user's."""
+    from epfl_megatron_amd.initialize import rccl_watchdog_env
+    env = {"TORCH_NCCL_ASYNC_ERROR_HANDLING": "1"}
+    got = rccl_watchdog_env(10, env)
+    assert got["TORCH_NCCL_ASYNC_ERROR_HANDLING"] == "1"
+    assert env["TORCH_NCCL_ENABLE_MONITORING"] == "1"
+    assert env["TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC"] == "600"
+    assert env["TORCH_NCCL_DUMP_ON_TIMEOUT"] == "1"
