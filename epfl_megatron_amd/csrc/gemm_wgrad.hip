@@ -34,10 +34,13 @@
 //     0: the first micro-batch of a step; main_grad is never zero-filled),
 //     transposed through LDS so G moves in 16-B row pieces (+1.5 % on fc1
 //     over per-lane 4-B accesses).
-//   * XCD-aware tile order: each XCD's consecutive tiles form 8 (n) x 4 (k)
-//     groups so concurrently running workgroups share operand panels in L2.
+//   * XCD-aware tile order: each XCD's consecutive tiles form 8 x 4 blocks
+//     (4 or 8 tiles of the shorter output dimension) so concurrently running
+//     workgroups share operand panels in L2.
 //
 // Shapes: N % 256 == 0, K % 256 == 0, M % 32 == 0 (checked by the host).
+#include <cstdlib>
+
 #include "fa_common.h"
 
 namespace ema {
@@ -111,7 +114,7 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
-        int K) {
+        int K, int gn) {
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -120,13 +123,23 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   // tile order: XCD-contiguous, then 8 (n) x 4 (k) groups
   const int ntn = N / TN, ntk = K / TK, ntiles = ntn * ntk;
   const int lin = xcd_remap(blockIdx.x, ntiles);
-  constexpr int GN = 8;
-  const int grp = lin / (GN * ntk);
-  const int first_n = grp * GN;
-  const int gsize = min(GN, ntn - first_n);
-  const int in_grp = lin - grp * GN * ntk;
-  const int tn = first_n + in_grp % gsize;
-  const int tk = in_grp / gsize;
+  int tn, tk;
+  if (gn > 0) {  // groups of gn n-tiles x all k-tiles, n fastest
+    const int grp = lin / (gn * ntk);
+    const int first_n = grp * gn;
+    const int gsize = min(gn, ntn - first_n);
+    const int in_grp = lin - grp * gn * ntk;
+    tn = first_n + in_grp % gsize;
+    tk = in_grp / gsize;
+  } else {       // groups of -gn k-tiles x all n-tiles, k fastest
+    const int gk = -gn;
+    const int grp = lin / (gk * ntn);
+    const int first_k = grp * gk;
+    const int gsize = min(gk, ntk - first_k);
+    const int in_grp = lin - grp * gk * ntn;
+    tk = first_k + in_grp % gsize;
+    tn = in_grp / gsize;
+  }
   const int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
 
   f32x4 acc[FA_][FB_];
@@ -360,11 +373,25 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   }
 }
 
+// Tile grouping: a few tiles of the SHORTER output dimension x all tiles of
+// the longer one, so an XCD's 32 concurrent workgroups form an 8 x 4 block
+// (measured on the 7B shapes, profiles/r2_wgrad_ab.txt: +3-5 % on qkv / fc1 /
+// lm_head over grouping along n).  EMA_WGRAD_GN overrides (> 0: groups of gn
+// n-tiles, < 0: groups of -gn k-tiles).
+int tile_group(int ntn, int ntk) {
+  static const int env = [] {
+    const char* e = getenv("EMA_WGRAD_GN");
+    return e ? atoi(e) : 0;
+  }();
+  if (env != 0) return env;
+  return ntn >= ntk ? -4 : 8;
+}
+
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s) {
   const int ntiles = (N / TN) * (K / TK);
   hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(ntiles), dim3(512), 0, s,
-                     (const T*)dy, (const T*)x, g, M, N, K);
+                     (const T*)dy, (const T*)x, g, M, N, K, tile_group(N / TN, K / TK));
 }
 
 }  // namespace
