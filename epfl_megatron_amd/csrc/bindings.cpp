@@ -504,6 +504,12 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   p.delta = delta.data_ptr<float>();
   p.ndelta = p.delta + b * nq * sq;
   p.lse2 = p.ndelta + b * nq * sq;
+  p.kv_split = ema::flash_attn_kv_split((int)b, (int)sk, (int)nq, (int)nkv);
+  at::Tensor ws;
+  if (p.kv_split > 1) {
+    ws = at::empty({(int64_t)p.kv_split * b * nkv * sk * 2 * hd}, q.options().dtype(at::kFloat));
+    p.dkv_ws = ws.data_ptr<float>();
+  }
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 

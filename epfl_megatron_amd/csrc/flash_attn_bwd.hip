@@ -513,8 +513,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, l4 = (lane >> 4) & 1;
-  const int nb = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
-  const int r = p.nq / p.nkv;
+  // blockIdx.y = KV group * kv_split + split: split takes query heads
+  // [split * r_per, (split + 1) * r_per) of the group
+  const int S = P.kv_split > 1 ? P.kv_split : 1;
+  const int nb = blockIdx.x, g = blockIdx.y / S, split = blockIdx.y % S, b = blockIdx.z;
+  const int r = p.nq / p.nkv, r_per = r / S, h0 = split * r_per;
   const int off = p.sk - p.sq;
   const int kbase = nb * BNK + wave * 32;
   const int key = kbase + c;
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
     q_first = q_first < 0 ? 0 : (q_first / BQ2) * BQ2;
   }
   const int nsteps_q = p.sq > q_first ? (p.sq - q_first + BQ2 - 1) / BQ2 : 0;
-  const int nsteps = r * nsteps_q;
+  const int nsteps = r_per * nsteps_q;
 
   // LDS-DMA source offsets of this lane's pieces (image (a) through the source)
   int srow[PPW], schunk[PPW];
@@ -542,8 +545,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
     schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
   }
   auto prefetch = [&](int step, int buf) {
-    const int hh = step / nsteps_q;
-    const int q0 = q_first + (step - hh * nsteps_q) * BQ2;
+    const int hl = step / nsteps_q, hh = h0 + hl;
+    const int q0 = q_first + (step - hl * nsteps_q) * BQ2;
     const int head = g * r + hh;
     const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)hh * p.q_sh;
     const T* DO = (const T*)P.dout + (int64_t)b * p.o_sb + (int64_t)head * p.o_sh;
@@ -596,8 +599,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
   __syncthreads();  // vmcnt(0) + barrier: step 0 landed
 
   for (int step = 0; step < nsteps; ++step) {
-    const int hh = step / nsteps_q;
-    const int q0 = q_first + (step - hh * nsteps_q) * BQ2;
+    const int hs = step / nsteps_q;
+    const int q0 = q_first + (step - hs * nsteps_q) * BQ2;
     const int buf = step & 1;
     if (step + 1 < nsteps) prefetch(step + 1, buf ^ 1);
     const char* bb = lds + buf * BUFB;
@@ -675,6 +678,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
   }
 
   mfma_drain();
+  if (S > 1) {  // fp32 partial sums; fa_dkv_reduce_k adds the splits in order
+    if (key < p.sk) {
+      float* W = P.dkv_ws + ((((int64_t)split * p.b + b) * p.nkv + g) * p.sk + key) * 2 * HD;
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          f4 wk, wv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            wk[e] = dk[d][4 * rg + e];
+            wv[e] = dv[d][4 * rg + e];
+          }
+          *reinterpret_cast<f4*>(W + d * 32 + 8 * rg + 4 * h) = wk;
+          *reinterpret_cast<f4*>(W + HD + d * 32 + 8 * rg + 4 * h) = wv;
+        }
+    }
+    return;
+  }
   if (key < p.sk) {
     T* DK = (T*)P.dk + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg + (int64_t)key * p.k_ss;
     T* DV = (T*)P.dv + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + (int64_t)key * p.v_ss;
@@ -693,6 +715,30 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
       }
     }
   }
+}
+
+// dK = scale * sum_s dK_s, dV = sum_s dV_s over the kv_split partial sums of
+// fa_bwd_dkdv2_k (fixed order: deterministic).  One thread = 4 elements.
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void fa_dkv_reduce_k(const AttnBwdParams P) {
+  const AttnParams& p = P.f;
+  const int64_t per = (int64_t)p.b * p.nkv * p.sk * (2 * HD / 4);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per) return;
+  const int c4 = (int)(t % (2 * HD / 4));
+  const int64_t row = t / (2 * HD / 4);  // (b, g, key)
+  const int key = (int)(row % p.sk), g = (int)((row / p.sk) % p.nkv), b = (int)(row / ((int64_t)p.sk * p.nkv));
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < P.kv_split; ++s)
+    acc += *reinterpret_cast<const f4*>(P.dkv_ws + ((int64_t)s * per + t) * 4);
+  const bool is_v = c4 * 4 >= HD;
+  const int col = c4 * 4 - (is_v ? HD : 0);
+  typename MT<T>::x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (T)(is_v ? acc[e] : acc[e] * p.scale);
+  T* dst = is_v ? (T*)P.dv + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + (int64_t)key * p.v_ss
+                : (T*)P.dk + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg + (int64_t)key * p.k_ss;
+  *reinterpret_cast<typename MT<T>::x4*>(dst + col) = o;
 }
 
 // dQ, v2: WAVES x 32 query rows of one head per workgroup (WAVES = 8: 512
@@ -875,6 +921,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   }
 }
 
+bool stamps_on() {
+  static const bool on = getenv("EMA_FA_STAMPS") != nullptr;
+  return on;
+}
+
 template <typename T, int HD>
 void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
   static const int ablate = [] {
@@ -886,7 +937,13 @@ void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
   const AttnParams& p = P.f;
   const int64_t rows = (int64_t)p.b * p.nq * p.sq;
   hipLaunchKernelGGL((fa_delta_k<T, HD>), dim3((rows + 255) / 256), dim3(256), 0, s, P);
-  const dim3 gkv((p.sk + BNK - 1) / BNK, p.nkv, p.b);
+  // dK/dV kernel: EMA_FA_DKDV = 1 (round-1 kernel) or 2 (64-row steps, LDS-DMA, default)
+  static const int kvv = [] {
+    const char* e = getenv("EMA_FA_DKDV");
+    return e ? atoi(e) : 2;
+  }();
+  if (kvv != 2 || stamps_on()) P.kv_split = 1;  // only the v2 kernel splits query heads
+  const dim3 gkv((p.sk + BNK - 1) / BNK, p.nkv * (P.kv_split > 1 ? P.kv_split : 1), p.b);
   const dim3 gq((p.sq + BMQ - 1) / BMQ, p.nq, p.b);
   // occupancy variants (waves/SIMD) for tuning: EMA_FA_BWD_OCC = "<dkdv><dq>", default "11"
   static const int occ = [] {
@@ -894,27 +951,28 @@ void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
     return e ? atoi(e) : 11;
   }();
   const bool kv2 = occ / 10 == 2, q2 = occ % 10 == 2;
+  const int64_t kvred = (int64_t)p.b * p.nkv * p.sk * (2 * HD / 4);
   // dQ kernel: EMA_FA_DQ = 1 (round-1 4-wave kernel) or 8 (8-wave, default)
   static const int dqv = [] {
     const char* e = getenv("EMA_FA_DQ");
     return e ? atoi(e) : 8;
   }();
   const dim3 gq2(((p.sq + 255) / 256) * p.nq * p.b);
-  // dK/dV kernel: EMA_FA_DKDV = 1 (round-1 kernel) or 2 (64-row steps, LDS-DMA, default)
-  static const int kvv = [] {
-    const char* e = getenv("EMA_FA_DKDV");
-    return e ? atoi(e) : 2;
-  }();
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
-    if (kvv == 2) hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P); \
+    if (kvv == 2) {                                                                       \
+      hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P);            \
+      if (P.kv_split > 1)                                                                 \
+        hipLaunchKernelGGL((fa_dkv_reduce_k<T, HD>), dim3((unsigned)((kvred + 255) / 256)), \
+                           dim3(256), 0, s, P);                                           \
+    }                                                                                     \
     else if (kv2) hipLaunchKernelGGL((fa_bwd_dkdv_k<T, HD, C, 2>), gkv, dim3(256), 0, s, P); \
     else hipLaunchKernelGGL((fa_bwd_dkdv_k<T, HD, C, 1>), gkv, dim3(256), 0, s, P);       \
     if (dqv == 8) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq2, dim3(512), 0, s, P); \
     else if (q2) hipLaunchKernelGGL((fa_bwd_dq_k<T, HD, C, 2>), gq, dim3(256), 0, s, P);  \
     else hipLaunchKernelGGL((fa_bwd_dq_k<T, HD, C, 1>), gq, dim3(256), 0, s, P);          \
   }
-  static const bool stamps = getenv("EMA_FA_STAMPS") != nullptr;
+  const bool stamps = stamps_on();
   if (stamps && p.causal) {  // diagnostic: per-segment cycle shares of the dK/dV loop
     const size_t nw = (size_t)gkv.x * gkv.y * gkv.z * 4;
     uint64_t* d = nullptr;

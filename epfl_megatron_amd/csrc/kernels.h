@@ -115,9 +115,23 @@ struct AttnBwdParams {
   float* delta;   // fp32 [b, nq, sq] workspace
   float* ndelta;  // fp32 [b, nq, sq]: -delta (initial dP accumulator of the v2 kernels)
   float* lse2;    // fp32 [b, nq, sq]: lse * log2(e)
+  float* dkv_ws;  // fp32 [kv_split][b][nkv][sk][2][hd] partial dK / dV (kv_split > 1)
+  int kv_split;    // query heads of a KV group split over this many dK/dV workgroups
   int ablate;     // profiling only (EMA_FA_ABLATE): bit 0 = no in-loop global prefetch
   uint64_t* stamps;  // diagnostic build only (EMA_FA_STAMPS)
 };
+// How many workgroups share one KV group's query heads in the dK/dV kernel:
+// the smallest divisor of r = nq / nkv that gives >= 512 workgroups (GQA/MQA
+// with few KV heads per rank, e.g. Llama-2-70B or Falcon-40B under TP, would
+// otherwise fill a quarter of the 256 CUs).  1 when nothing is gained.
+inline int flash_attn_kv_split(int b, int sk, int nq, int nkv) {
+  const int r = nq / nkv;
+  const long base = (long)((sk + 127) / 128) * nkv * b;
+  if (r <= 1 || base >= 512) return 1;
+  for (int s = 2; s <= r; ++s)
+    if (r % s == 0 && base * s >= 512) return s;
+  return r;
+}
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
