@@ -2,7 +2,7 @@
 # PMC passes over the wgrad kernel (fc1 shape), full and no-load ablation.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
-for MODE in 0 2; do
+for MODE in 20 22; do
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmcwg${MODE}_t -o w -- python3 scripts/wgrad_once.py 22016 4096 $MODE > gpurun_out/pmcwg_t.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-trace --output-format csv -d gpurun_out/pmcwg${MODE}_1 -o w -- python3 scripts/wgrad_once.py 22016 4096 $MODE > gpurun_out/pmcwg_1.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_ACTIVE_INST_LDS --kernel-trace --output-format csv -d gpurun_out/pmcwg${MODE}_2 -o w -- python3 scripts/wgrad_once.py 22016 4096 $MODE > gpurun_out/pmcwg_2.log 2>&1 || exit 1
