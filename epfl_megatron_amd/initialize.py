@@ -75,7 +75,8 @@ def _initialize_distributed(args):
         local_rank = int(os.environ.get("LOCAL_RANK", args.rank % max(torch.cuda.device_count(), 1)))
         if args.local_rank is not None and args.local_rank != local_rank:
             local_rank = args.local_rank
-        torch.cuda.set_device(local_rank)
+        # modulo: a rehearsal with more ranks than visible GPUs shares devices
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
         args.local_rank = local_rank
     backend = args.distributed_backend if use_gpu else "gloo"
     args.distributed_backend = backend
