@@ -163,7 +163,8 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
 
 // ---------------------------------------------------------------- rope
 void rope_qkv_inplace(at::Tensor qkv5, const at::Tensor& cos, const at::Tensor& sin,
-                      const c10::optional<at::Tensor>& pos, int64_t offset, bool inverse) {
+                      const c10::optional<at::Tensor>& pos, int64_t offset, bool inverse,
+                      bool k_only) {
   check_gpu(qkv5, "qkv");
   TORCH_CHECK(qkv5.dim() == 5, "qkv must be [s, b, ng, r+2, hd]");
   TORCH_CHECK(qkv5.stride(4) == 1, "head_dim must be contiguous");
@@ -189,8 +190,8 @@ void rope_qkv_inplace(at::Tensor qkv5, const at::Tensor& cos, const at::Tensor& 
   }
   ema::rope_qkv_inplace(qkv5.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pp, psb,
                         S, B, G, R, HD, qkv5.stride(0), qkv5.stride(1), qkv5.stride(2),
-                        qkv5.stride(3), (int)offset, inverse ? 1 : 0, dtype_code(qkv5),
-                        cur_stream());
+                        qkv5.stride(3), (int)offset, inverse ? 1 : 0, k_only ? 1 : 0,
+                        dtype_code(qkv5), cur_stream());
 }
 
 // ---------------------------------------------------------------- activations
@@ -476,12 +477,41 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   return p;
 }
 
+// Fused RoPE tables for the attention kernels (see AttnParams): fp32
+// [max_pos, hd/2] cos/sin, optional int64 [b, s] position ids (else the row
+// index is the position, sq == sk).
+static void set_rope(ema::AttnParams& p, const c10::optional<at::Tensor>& cos,
+                     const c10::optional<at::Tensor>& sin, const c10::optional<at::Tensor>& pos) {
+  if (!(cos.has_value() && cos->defined())) return;
+  TORCH_CHECK(sin.has_value() && sin->defined(), "rope needs both cos and sin");
+  TORCH_CHECK(cos->scalar_type() == at::kFloat && sin->scalar_type() == at::kFloat &&
+              cos->is_contiguous() && sin->is_contiguous() && cos->dim() == 2 &&
+              cos->sizes() == sin->sizes(), "rope tables must be contiguous fp32 [max_pos, hd/2]");
+  TORCH_CHECK(cos->size(1) == p.hd / 2, "rope table width must be head_dim / 2");
+  TORCH_CHECK(p.sq == p.sk, "fused rope needs sq == sk");
+  check_gpu(*cos, "rope_cos");
+  p.rope_cos = cos->data_ptr<float>();
+  p.rope_sin = sin->data_ptr<float>();
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->dim() == 2 && pos->size(0) == p.b &&
+                pos->size(1) == p.sq && pos->stride(1) == 1, "position_ids must be int64 [b, s]");
+    p.rope_pos = pos->data_ptr<int64_t>();
+    p.rope_pos_sb = pos->stride(0);
+  } else {
+    TORCH_CHECK(p.sq <= cos->size(0), "rope table too short for sequence");
+  }
+}
+
 void flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
                     at::Tensor lse, int64_t b, int64_t sq, int64_t sk, int64_t nq, int64_t nkv,
                     int64_t hd, std::vector<int64_t> qs, std::vector<int64_t> ks,
-                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale) {
+                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale,
+                    const c10::optional<at::Tensor>& rope_cos,
+                    const c10::optional<at::Tensor>& rope_sin,
+                    const c10::optional<at::Tensor>& rope_pos) {
   check_gpu(q, "q");
   auto p = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  set_rope(p, rope_cos, rope_sin, rope_pos);
   ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
 }
 
@@ -489,9 +519,13 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
                     const at::Tensor& v, const at::Tensor& out, const at::Tensor& lse, at::Tensor dq,
                     at::Tensor dk, at::Tensor dv, int64_t b, int64_t sq, int64_t sk, int64_t nq,
                     int64_t nkv, int64_t hd, std::vector<int64_t> qs, std::vector<int64_t> ks,
-                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale) {
+                    std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale,
+                    const c10::optional<at::Tensor>& rope_cos,
+                    const c10::optional<at::Tensor>& rope_sin,
+                    const c10::optional<at::Tensor>& rope_pos) {
   check_gpu(q, "q");
   auto f = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  set_rope(f, rope_cos, rope_sin, rope_pos);
   TORCH_CHECK(dout.scalar_type() == q.scalar_type(), "dout dtype mismatch");
   TORCH_CHECK(dout.stride(-1) == 1, "dout head_dim must be contiguous");
   ema::AttnBwdParams p{};

@@ -156,6 +156,44 @@ __device__ __forceinline__ typename MT<T>::x8 acc_frag(const f32x16& acc, int s)
 
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
+// ---- fused RoPE (Meta-Llama interleaved pairs (x[2j], x[2j+1]), fp32) ------
+typedef __attribute__((ext_vector_type(2))) float rf2;
+typedef __attribute__((ext_vector_type(4))) float rf4;
+
+// Table rows (cos, sin) of sequence row `row` of batch `b`.
+template <int HD>
+__device__ __forceinline__ void rope_rows(const AttnParams& p, int b, int row, const float*& c,
+                                          const float*& s) {
+  const int64_t pos = p.rope_pos ? p.rope_pos[(int64_t)b * p.rope_pos_sb + row] : (int64_t)row;
+  c = p.rope_cos + pos * (HD / 2);
+  s = p.rope_sin + pos * (HD / 2);
+}
+// R^T on 4 consecutive fp32 elements starting at head-dim index 2*j0 (j0 even).
+__device__ __forceinline__ void rope_inv4(float (&x)[4], const float* c, const float* s, int j0) {
+  const rf2 cc = *reinterpret_cast<const rf2*>(c + j0);
+  const rf2 sn = *reinterpret_cast<const rf2*>(s + j0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float x0 = x[2 * i], x1 = x[2 * i + 1];
+    x[2 * i] = x0 * cc[i] + x1 * sn[i];
+    x[2 * i + 1] = x1 * cc[i] - x0 * sn[i];
+  }
+}
+// R on an 8-element 16-bit fragment starting at head-dim index 2*j0 (j0 % 4 == 0).
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x8 rope_fwd8(typename MT<T>::x8 v, const float* c,
+                                                        const float* s, int j0) {
+  const rf4 cc = *reinterpret_cast<const rf4*>(c + j0);
+  const rf4 sn = *reinterpret_cast<const rf4*>(s + j0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = (float)v[2 * i], x1 = (float)v[2 * i + 1];
+    v[2 * i] = (T)(x0 * cc[i] - x1 * sn[i]);
+    v[2 * i + 1] = (T)(x0 * sn[i] + x1 * cc[i]);
+  }
+  return v;
+}
+
 // 16-byte-chunk XOR swizzle for [rows][HD] tiles that are read both by rows
 // (ds_read_b128 A/B fragments) and transposed (ds_read_b64_tr_b16): CDNA guide
 // T10 image (b) for 256-byte rows; a 3-bit analogue for 128-byte rows.

@@ -29,11 +29,12 @@ void layernorm_bwd(const void* dy, const void* x, const void* w, const float* me
 
 // ---- rope.hip ----------------------------------------------------------------
 // In-place rotation of q (r heads per group) and k (1 head per group) of a
-// [s, b, ng, r+2, hd] tensor with element strides (ss, sb, sg, sh).
+// [s, b, ng, r+2, hd] tensor with element strides (ss, sb, sg, sh); k_only:
+// the key heads only.
 void rope_qkv_inplace(void* qkv, const float* cos, const float* sin, const int64_t* pos,
                       int64_t pos_stride_b, int S, int B, int G, int R, int HD, int64_t ss,
-                      int64_t sb, int64_t sg, int64_t sh, int offset, int inverse, int dt,
-                      hipStream_t s);
+                      int64_t sb, int64_t sg, int64_t sh, int offset, int inverse, int k_only,
+                      int dt, hipStream_t s);
 
 // ---- activations.hip -----------------------------------------------------------
 void glu_fwd(const void* x, void* y, int64_t rows, int F, int kind, int dt, hipStream_t s);
@@ -105,6 +106,13 @@ struct AttnParams {
   int64_t o_sb, o_ss, o_sh;  // o / dout share strides
   int causal;
   float scale;
+  // Optional fused RoPE (interleaved pairs, fp32 tables [max_pos, hd/2]):
+  // forward rotates Q in registers and writes it back in place (the block
+  // that owns the rows); backward applies R^T to dQ and dK in its epilogues.
+  const float* rope_cos;
+  const float* rope_sin;
+  const int64_t* rope_pos;  // [b, s] position ids (row stride rope_pos_sb) or null: row index
+  int64_t rope_pos_sb;
 };
 struct AttnBwdParams {
   AttnParams f;
@@ -117,8 +125,6 @@ struct AttnBwdParams {
   float* lse2;    // fp32 [b, nq, sq]: lse * log2(e)
   float* dkv_ws;  // fp32 [kv_split][b][nkv][sk][2][hd] partial dK / dV (kv_split > 1)
   int kv_split;    // query heads of a KV group split over this many dK/dV workgroups
-  int ablate;     // profiling only (EMA_FA_ABLATE): bit 0 = no in-loop global prefetch
-  uint64_t* stamps;  // diagnostic build only (EMA_FA_STAMPS)
 };
 // How many workgroups share one KV group's query heads in the dK/dV kernel:
 // the smallest divisor of r = nq / nkv that gives >= 512 workgroups (GQA/MQA

@@ -5,7 +5,10 @@
 // (reference megatron/model/positional_embeddings.py:24-51).  The r query
 // heads and the single key head of every group are rotated; v is untouched.
 // Each thread handles 8 consecutive elements (one 16-byte bf16 vector =
-// 4 pairs); `inverse` applies R^T (used on dQ/dK in the backward pass).
+// 4 pairs); `inverse` applies R^T.  `k_only` rotates just the key head of
+// every group: the training path rotates Q inside the FlashAttention forward
+// and un-rotates dQ/dK in the FlashAttention backward epilogues, so only K
+// needs this pass there.
 #include "common.h"
 #include "kernels.h"
 
@@ -18,14 +21,15 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* 
                                               const int64_t* __restrict__ pos, int64_t pos_sb,
                                               int S, int B, int G, int R, int HD, int64_t ss,
                                               int64_t sb, int64_t sg, int64_t sh, int offset,
-                                              int inverse, int64_t total) {
+                                              int inverse, int k_only, int64_t total) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int nv = HD / 8;                 // 8-element vectors per head
   const int d8 = (int)(t % nv);
   int64_t rest = t / nv;
-  const int h = (int)(rest % (R + 1));   // 0..R-1 query heads, R = key head
-  rest /= (R + 1);
+  const int nh = k_only ? 1 : R + 1;
+  const int h = (k_only ? R : 0) + (int)(rest % nh);  // 0..R-1 query heads, R = key head
+  rest /= nh;
   const int g = (int)(rest % G);
   rest /= G;
   const int b = (int)(rest % B);
@@ -64,14 +68,14 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* 
 
 void rope_qkv_inplace(void* qkv, const float* cos, const float* sin, const int64_t* pos,
                       int64_t pos_stride_b, int S, int B, int G, int R, int HD, int64_t ss,
-                      int64_t sb, int64_t sg, int64_t sh, int offset, int inverse, int dt,
-                      hipStream_t s) {
-  const int64_t total = (int64_t)S * B * G * (R + 1) * (HD / 8);
+                      int64_t sb, int64_t sg, int64_t sh, int offset, int inverse, int k_only,
+                      int dt, hipStream_t s) {
+  const int64_t total = (int64_t)S * B * G * (k_only ? 1 : R + 1) * (HD / 8);
   if (total == 0) return;
   const int64_t blocks = (total + 255) / 256;
   EMA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((rope_k<T>), dim3(blocks), dim3(256), 0, s,
                                                (T*)qkv, cos, sin, pos, pos_stride_b, S, B, G, R,
-                                               HD, ss, sb, sg, sh, offset, inverse, total));
+                                               HD, ss, sb, sg, sh, offset, inverse, k_only, total));
 }
 
 }  // namespace ema

@@ -3,13 +3,16 @@
 ``flash_attn_qkvpacked`` is the training hot path: it takes the fused QKV
 projection output in the reference's GQA layout ``[s, b, ng, r+2, hd]``
 (r = nq/nkv query heads per KV group, then k, then v;
-reference ``megatron/model/transformer.py:445-455``), applies RoPE in place,
-and runs the hand-written gfx950 FlashAttention-2 kernel
+reference ``megatron/model/transformer.py:445-455``) and runs the
+hand-written gfx950 FlashAttention-2 kernel
 (``csrc/flash_attn_fwd.hip`` / ``flash_attn_bwd.hip``) reading Q/K/V through
 strides.  GQA/MQA is native: query head ``j`` reads KV group ``j // r``; K/V
 are never expanded to ``nq`` heads (the reference broadcast them, D2).
-The backward writes dQ/dK/dV straight into a ``[s, b, ng, r+2, hd]`` gradient
-buffer, un-rotates dQ/dK in place, and hands it to the QKV GEMM backward.
+RoPE is fused: a k-only pass rotates the key heads, the forward kernel
+rotates Q in registers (and writes it back for the backward), and the
+backward kernels apply R^T to dQ/dK in their epilogues while writing them
+straight into a ``[s, b, ng, r+2, hd]`` gradient buffer for the QKV GEMM
+backward.
 
 ``flash_attn_func`` is the general entry (separate q/k/v, ``sq <= sk`` with
 bottom-right-aligned causal mask) used by KV-cached inference.
@@ -92,15 +95,18 @@ class _FlashQKVPackedFn(torch.autograd.Function):
     def forward(ctx, qkv, ng, r, hd, causal, scale, cos, sin, position_ids):
         s, b = qkv.shape[0], qkv.shape[1]
         qkv5 = qkv.view(s, b, ng, r + 2, hd)
-        if cos is not None:
-            rope_qkv_inplace(qkv5, cos, sin, position_ids)
+        if position_ids is not None and position_ids.dtype != torch.int64:
+            position_ids = position_ids.long()
+        if cos is not None:  # keys only: Q is rotated inside the attention kernel
+            rope_qkv_inplace(qkv5, cos, sin, position_ids, k_only=True)
         q, k, v, qs, ks = _qkv5_views(qkv5)
         nq = ng * r
         out = torch.empty(s, b, nq, hd, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(b, nq, s, dtype=torch.float32, device=qkv.device)
         os_ = (out.stride(1), out.stride(0), out.stride(2))
         ext().flash_attn_fwd(q, k, v, out, lse, b, s, s, nq, ng, hd,
-                             list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale))
+                             list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale),
+                             cos, sin, position_ids)
         ctx.save_for_backward(qkv, out, lse, cos, sin, position_ids)
         ctx.meta = (ng, r, hd, causal, scale)
         return out.view(s, b, nq * hd)
@@ -120,9 +126,8 @@ class _FlashQKVPackedFn(torch.autograd.Function):
         dq, dk, dv, _, _ = _qkv5_views(dqkv5)
         os_ = (out.stride(1), out.stride(0), out.stride(2))
         ext().flash_attn_bwd(dout, q, k, v, out, lse, dq, dk, dv, b, s, s, nq, ng, hd,
-                             list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale))
-        if cos is not None:
-            rope_qkv_inplace(dqkv5, cos, sin, position_ids, inverse=True)
+                             list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale),
+                             cos, sin, position_ids)
         return dqkv5.view(s, b, -1), None, None, None, None, None, None, None, None
 
 
@@ -141,7 +146,8 @@ class _FlashFn(torch.autograd.Function):
         vs = _bsnd_strides(v, 1)[:3]
         os_ = (out.stride(0), out.stride(1), out.stride(2))
         ext().flash_attn_fwd(q, k, v, out, lse, b, sq, sk, nq, nkv, d,
-                             list(qs), list(ks), list(vs), list(os_), bool(causal), float(scale))
+                             list(qs), list(ks), list(vs), list(os_), bool(causal), float(scale),
+                             None, None, None)
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.causal, ctx.scale = causal, scale
         return out
@@ -160,7 +166,7 @@ class _FlashFn(torch.autograd.Function):
         os_ = (out.stride(0), out.stride(1), out.stride(2))
         ext().flash_attn_bwd(dout, q, k, v, out, lse, dq, dk, dv, b, sq, sk, nq, nkv, d,
                              list(qs), list(ks), list(ks), list(os_), bool(ctx.causal),
-                             float(ctx.scale))
+                             float(ctx.scale), None, None, None)
         return dq, dk, dv, None, None
 
 

@@ -62,21 +62,24 @@ def apply_rope_ref(x, cos, sin, position_ids=None, offset=0, inverse=False):
     return out.type_as(x)
 
 
-def rope_qkv_inplace(qkv5, cos, sin, position_ids=None, offset=0, inverse=False):
-    """Rotate q and k heads of a fused ``[s, b, ng, r+2, hd]`` tensor in place.
+def rope_qkv_inplace(qkv5, cos, sin, position_ids=None, offset=0, inverse=False,
+                     k_only=False):
+    """Rotate q and k heads (``k_only``: just the key heads) of a fused
+    ``[s, b, ng, r+2, hd]`` tensor in place.
 
     Not an autograd op: callers (the attention Function) own the gradient."""
     if use_native(qkv5):
         pos = position_ids
         if pos is not None and pos.dtype != torch.int64:
             pos = pos.long()
-        ext().rope_qkv_inplace(qkv5, cos, sin, pos, int(offset), bool(inverse))
+        ext().rope_qkv_inplace(qkv5, cos, sin, pos, int(offset), bool(inverse), bool(k_only))
         return qkv5
     r2 = qkv5.shape[3]
     s, b, ng, _, hd = qkv5.shape
-    qk = qkv5[:, :, :, :r2 - 1, :].reshape(s, b, ng * (r2 - 1), hd)
+    lo = r2 - 2 if k_only else 0
+    qk = qkv5[:, :, :, lo:r2 - 1, :].reshape(s, b, ng * (r2 - 1 - lo), hd)
     rot = apply_rope_ref(qk, cos, sin, position_ids, offset, inverse)
-    qkv5[:, :, :, :r2 - 1, :].copy_(rot.view(s, b, ng, r2 - 1, hd))
+    qkv5[:, :, :, lo:r2 - 1, :].copy_(rot.view(s, b, ng, r2 - 1 - lo, hd))
     return qkv5
 
 

@@ -1,7 +1,6 @@
 """FlashAttention forward/backward timing on the training shapes (1 GPU).
 
-Usage: python scripts/fa_bench2.py [b,s,nq,nkv,hd ...]   (EMA_FA_FWD selects the
-forward variant).  Median of 10 timed launches after 3 warm-up launches, random
+Usage: python scripts/fa_bench2.py [b,s,nq,nkv,hd ...].  Median of 10 timed launches after 3 warm-up launches, random
 data, causal; TF/s counts the causal half (4*b*nq*s^2*hd/2 fwd, 2.5x that bwd).
 """
 import os
@@ -37,7 +36,7 @@ def bench(b, s, nq, nkv, hd):
             tb.append(e[1].elapsed_time(e[2]))
         q.grad = k.grad = v.grad = None
     mf, mb = statistics.median(tf), statistics.median(tb)
-    print(f"variant={os.environ.get('EMA_FA_FWD', 'default')} shape={b},{s},{nq},{nkv},{hd}: "
+    print(f"shape={b},{s},{nq},{nkv},{hd}: "
           f"fwd {mf * 1e3:.1f} us {fl / mf / 1e9:.0f} TF/s | bwd {mb * 1e3:.1f} us "
           f"{2.5 * fl / mb / 1e9:.0f} TF/s", flush=True)
 

@@ -14,7 +14,5 @@ timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 ||
 grep smoke gpurun_out/smoke.log
 timeout -k 10 900 python bench.py --steps 8 --warmup 3 > gpurun_out/bench_7b.log 2>&1 || { tail -30 gpurun_out/bench_7b.log; exit 1; }
 tail -1 gpurun_out/bench_7b.log
-for v in 1 8; do
-  EMA_FA_FWD=$v timeout -k 10 200 python scripts/fa_bench2.py > gpurun_out/fa_bench_v$v.log 2>&1 || { tail -20 gpurun_out/fa_bench_v$v.log; exit 1; }
-  grep variant gpurun_out/fa_bench_v$v.log
-done
+timeout -k 10 200 python scripts/fa_bench2.py > gpurun_out/fa_bench.log 2>&1 || { tail -20 gpurun_out/fa_bench.log; exit 1; }
+grep shape gpurun_out/fa_bench.log

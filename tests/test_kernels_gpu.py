@@ -328,17 +328,27 @@ def test_flash_attention_fp16():
     _attn_case(1, 192, 4, 4, 128, torch.float16, True)
 
 
-def test_flash_attention_qkvpacked_rope():
-    """The training path: fused GQA QKV + in-place RoPE + FA, fwd and bwd."""
+@pytest.mark.parametrize("s,b,ng,r,hd,with_pos", [
+    (300, 2, 2, 3, 128, False),   # GQA, dK/dV split over query heads (reduce-kernel epilogue)
+    (4096, 1, 2, 1, 128, False),  # Llama-2 native context, MHA (dK/dV kernel epilogue)
+    (257, 2, 1, 8, 64, True),     # Falcon-like MQA, head_dim 64, explicit position ids
+])
+def test_flash_attention_qkvpacked_rope(s, b, ng, r, hd, with_pos):
+    """The training path: fused GQA QKV + RoPE fused into FA (k-only rotation
+    pass, Q rotated in the forward kernel, R^T on dQ/dK in the backward
+    epilogues), fwd and bwd against the fp32 CPU reference."""
     from epfl_megatron_amd.ops.attention import flash_attn_qkvpacked
     from epfl_megatron_amd.ops.rope import rope_table
-    torch.manual_seed(9)
-    s, b, ng, r, hd = 300, 2, 2, 3, 128
-    cos, sin = rope_table(hd, 512, DEV)
+    torch.manual_seed(9 + s)
+    cos, sin = rope_table(hd, 8192, DEV)
+    pos = None
+    if with_pos:
+        pos = (torch.arange(s)[None, :] + torch.tensor([[3], [700]])[:b]).to(DEV)
     x = torch.randn(s, b, ng * (r + 2) * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    o = flash_attn_qkvpacked(x.clone(), ng, r, hd, causal=True, rope=(cos, sin))
+    o = flash_attn_qkvpacked(x.clone(), ng, r, hd, causal=True, rope=(cos, sin), position_ids=pos)
     xr = x.detach().float().cpu().requires_grad_()
-    orf = flash_attn_qkvpacked(xr, ng, r, hd, causal=True, rope=(cos.cpu(), sin.cpu()))
+    orf = flash_attn_qkvpacked(xr, ng, r, hd, causal=True, rope=(cos.cpu(), sin.cpu()),
+                               position_ids=None if pos is None else pos.cpu())
     _close(o.cpu(), orf, 3e-2, 3e-2, "qkvpacked fwd")
     g = torch.randn_like(o)
     o.backward(g)
