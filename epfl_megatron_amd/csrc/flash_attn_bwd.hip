@@ -529,14 +529,17 @@ void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
   hipLaunchKernelGGL((fa_delta_k<T, HD>), dim3((rows + 255) / 256), dim3(256), 0, s, P);
   const dim3 gkv((p.sk + BNK - 1) / BNK, p.nkv * (P.kv_split > 1 ? P.kv_split : 1), p.b);
   const int64_t kvred = (int64_t)p.b * p.nkv * p.sk * (2 * HD / 4);
+  const int wv = flash_attn_waves(p.b, p.sq, p.nq, HD);
   const dim3 gq(((p.sq + 255) / 256) * p.nq * p.b);
+  const dim3 gq4(((p.sq + 127) / 128) * p.nq * p.b);
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
     hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P);              \
     if (P.kv_split > 1)                                                                   \
       hipLaunchKernelGGL((fa_dkv_reduce_k<T, HD>), dim3((unsigned)((kvred + 255) / 256)), \
                          dim3(256), 0, s, P);                                             \
-    hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq, dim3(512), 0, s, P);              \
+    if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \
+    else hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq, dim3(512), 0, s, P);         \
   }
   if (p.causal) EMA_FA_BWD(true) else EMA_FA_BWD(false)
 #undef EMA_FA_BWD

@@ -22,6 +22,8 @@
 // Fused RoPE (p.rope_cos set): Q is rotated in registers right after its load
 // and written back in place (only this workgroup reads those rows), so the
 // backward sees rotated Q; K is rotated by a k-only pre-pass (rope.hip).
+#include <cstdlib>
+
 #include "fa_common.h"
 #include "kernels.h"
 
@@ -266,13 +268,24 @@ bool flash_attn_supported(int hd, int dt) {
   return (hd == 64 || hd == 128) && (dt == DT_BF16 || dt == DT_F16);
 }
 
+int flash_attn_waves(int b, int sq, int nq, int hd) {
+  static const int forced = [] {
+    const char* e = getenv("EMA_FA_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 4 || forced == 8) return forced;
+  const long blocks8 = (long)((sq + 255) / 256) * nq * b;
+  return (hd == 64 || blocks8 < 512) ? 4 : 8;
+}
+
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
+  const bool w4 = flash_attn_waves(p.b, p.sq, p.nq, p.hd) == 4;
   if (dt == DT_BF16) {
-    if (p.hd == 128) fa::launch_fwd2<bf16, 128, 8>(p, s);
-    else fa::launch_fwd2<bf16, 64, 8>(p, s);
+    if (p.hd == 128) w4 ? fa::launch_fwd2<bf16, 128, 4>(p, s) : fa::launch_fwd2<bf16, 128, 8>(p, s);
+    else w4 ? fa::launch_fwd2<bf16, 64, 4>(p, s) : fa::launch_fwd2<bf16, 64, 8>(p, s);
   } else {
-    if (p.hd == 128) fa::launch_fwd2<fp16, 128, 8>(p, s);
-    else fa::launch_fwd2<fp16, 64, 8>(p, s);
+    if (p.hd == 128) w4 ? fa::launch_fwd2<fp16, 128, 4>(p, s) : fa::launch_fwd2<fp16, 128, 8>(p, s);
+    else w4 ? fa::launch_fwd2<fp16, 64, 4>(p, s) : fa::launch_fwd2<fp16, 64, 8>(p, s);
   }
 }
 

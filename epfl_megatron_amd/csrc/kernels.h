@@ -138,6 +138,11 @@ inline int flash_attn_kv_split(int b, int sk, int nq, int nkv) {
     if (r % s == 0 && base * s >= 512) return s;
   return r;
 }
+// Waves per forward / dQ workgroup: 8 (256 query rows, one block per CU) on
+// big grids, 4 (128 rows, two blocks per CU) at head_dim 64 and when the
+// 8-wave grid would give fewer than two blocks per CU (few heads per TP rank):
+// profiles/r2c_fa_waves_ab.txt.  EMA_FA_WAVES=4|8 overrides.
+int flash_attn_waves(int b, int sq, int nq, int hd);
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
