@@ -77,46 +77,63 @@ __global__ __launch_bounds__(256) void fa_delta_k(const AttnBwdParams P) {
 // hipcc does not drain the in-flight DMA in front of them.
 constexpr int BQ2 = 64;
 
+// Persistent form: a flat grid of min(items, CUs) workgroups walks the
+// (key block, KV group x split, batch) items, listed heaviest-first, in a
+// snake order (round k: item k*G + w, or k*G + G-1-w for odd k), so under the
+// causal mask every workgroup gets a balanced sum of work.  Across an item seam the next item's K/V rows (LDS-DMA into a
+// staging image, read into registers at the item start) and its first Q/dO
+// step are loaded during the current item's steps, so the per-item prologue
+// (≈ 4-5 steps' worth of load latency at s = 1024) is hidden.
 template <typename T, int HD, bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) {
   typedef typename MT<T>::x8 x8;
   typedef typename MT<T>::x4 x4;
   const AttnParams& p = P.f;
-  constexpr int KS = HD / 16, DT = HD / 32;
-  constexpr int ROWB = HD * 2;                   // bytes per Q / dO row
+  constexpr int KS = HD / 16, DT = HD / 32, CH = HD / 8;
+  constexpr int ROWB = HD * 2;                   // bytes per Q / dO / K / V row
   constexpr int RG = 8 * ROWB;                   // bytes per 8-row group (image (a))
   constexpr int TILEB = BQ2 * ROWB;              // one Q (or dO) tile
   constexpr int BUFB = 2 * TILEB + 2 * BQ2 * 4;  // Q, dO, lse2, -delta
   constexpr int PIECES = TILEB / 1024, PPW = PIECES / 4;
-  static_assert(PIECES % 4 == 0, "pieces per wave");
-  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
+  constexpr int KVB = BNK * ROWB;                // K (or V) rows of one item
+  constexpr int KVPW = KVB / 1024 / 4;           // 1-KiB DMA pieces per wave for K (and V)
+  static_assert(PIECES % 4 == 0 && (KVB / 1024) % 4 == 0, "pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB + 2 * KVB];
+  char* const kvs = lds + 2 * BUFB;  // staging: K rows then V rows, chunk ^ (row % CH)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, l4 = (lane >> 4) & 1;
-  // blockIdx.y = KV group * kv_split + split: split takes query heads
-  // [split * r_per, (split + 1) * r_per) of the group
   const int S = P.kv_split > 1 ? P.kv_split : 1;
-  const int nb = blockIdx.x, g = blockIdx.y / S, split = blockIdx.y % S, b = blockIdx.z;
-  const int r = p.nq / p.nkv, r_per = r / S, h0 = split * r_per;
+  const int r = p.nq / p.nkv, r_per = r / S;
   const int off = p.sk - p.sq;
-  const int kbase = nb * BNK + wave * 32;
-  const int key = kbase + c;
-  const int key_c = key < p.sk ? key : p.sk - 1;
   const float sl2 = p.scale * 1.4426950408889634f;
+  const int ngs = p.nkv * S;
+  const int nitems = ((p.sk + BNK - 1) / BNK) * ngs * p.b;
 
-  const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
-  const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
+  // item -> key block (heaviest first), KV group, query-head split, batch
+  struct Item {
+    int nb, g, split, b, h0, q_first, nsteps_q, nsteps;
+  };
+  auto decode = [&](int it, Item& I) {
+    I.nb = it / (ngs * p.b);
+    const int rem = it - I.nb * (ngs * p.b);
+    const int gs = rem % ngs;
+    I.b = rem / ngs;
+    I.g = gs / S;
+    I.split = gs % S;
+    I.h0 = I.split * r_per;
+    int qf = 0;
+    if (CAUSAL) {
+      qf = I.nb * BNK - off;
+      qf = qf < 0 ? 0 : (qf / BQ2) * BQ2;
+    }
+    I.q_first = qf;
+    I.nsteps_q = p.sq > qf ? (p.sq - qf + BQ2 - 1) / BQ2 : 0;
+    I.nsteps = r_per * I.nsteps_q;
+  };
 
-  int q_first = 0;
-  if (CAUSAL) {
-    q_first = nb * BNK - off;
-    q_first = q_first < 0 ? 0 : (q_first / BQ2) * BQ2;
-  }
-  const int nsteps_q = p.sq > q_first ? (p.sq - q_first + BQ2 - 1) / BQ2 : 0;
-  const int nsteps = r_per * nsteps_q;
-
-  // LDS-DMA source offsets of this lane's pieces (image (a) through the source)
+  // LDS-DMA source offsets of this lane's Q/dO pieces (image (a) through the source)
   int srow[PPW], schunk[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -125,12 +142,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
     srow[i] = 8 * (o / RG) + rem2 / 64;
     schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
   }
-  auto prefetch = [&](int step, int buf) {
-    const int hl = step / nsteps_q, hh = h0 + hl;
-    const int q0 = q_first + (step - hl * nsteps_q) * BQ2;
-    const int head = g * r + hh;
-    const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)hh * p.q_sh;
-    const T* DO = (const T*)P.dout + (int64_t)b * p.o_sb + (int64_t)head * p.o_sh;
+  auto prefetch = [&](const Item& I, int step, int buf) {
+    const int hl = step / I.nsteps_q, hh = I.h0 + hl;
+    const int q0 = I.q_first + (step - hl * I.nsteps_q) * BQ2;
+    const int head = I.g * r + hh;
+    const T* Q = (const T*)p.q + (int64_t)I.b * p.q_sb + (int64_t)I.g * p.q_sg + (int64_t)hh * p.q_sh;
+    const T* DO = (const T*)P.dout + (int64_t)I.b * p.o_sb + (int64_t)head * p.o_sh;
     char* base = lds + buf * BUFB;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -147,14 +164,37 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
     if (wave < 2) {  // 64 rows x 4 B: one dword-wide piece each for lse2 and -delta
       int qr = q0 + lane;
       qr = qr < p.sq ? qr : p.sq - 1;
-      const int64_t rb = ((int64_t)b * p.nq + head) * p.sq;
+      const int64_t rb = ((int64_t)I.b * p.nq + head) * p.sq;
       const float* src = wave == 0 ? P.lse2 + rb + qr : P.ndelta + rb + qr;
       __builtin_amdgcn_global_load_lds(
           (const void*)src,
           (__attribute__((address_space(3))) void*)(base + 2 * TILEB + wave * BQ2 * 4), 4, 0, 0);
     }
   };
-  if (nsteps > 0) prefetch(0, 0);
+  // K / V rows of an item into the staging image: piece byte o holds row
+  // o / ROWB, physical chunk (o % ROWB) / 16 = logical chunk ^ (row % CH).
+  auto kv_prefetch = [&](const Item& I) {
+    const T* K = (const T*)p.k + (int64_t)I.b * p.k_sb + (int64_t)I.g * p.k_sg;
+    const T* V = (const T*)p.v + (int64_t)I.b * p.v_sb + (int64_t)I.g * p.v_sg;
+    // lane index made opaque: the piece addresses are recomputed here (twice
+    // per item) instead of being hoisted and held in 32 VGPRs across the loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int i = 0; i < KVPW; ++i) {
+      const int pc = wave * KVPW + i;
+      const int o = pc * 1024 + 16 * ln;
+      const int row = o / ROWB, ch = ((o % ROWB) / 16) ^ (row % CH);
+      int kr = I.nb * BNK + row;
+      kr = kr < p.sk ? kr : p.sk - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(K + (int64_t)kr * p.k_ss + ch * 8),
+                                       (__attribute__((address_space(3))) void*)(kvs + pc * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(V + (int64_t)kr * p.v_ss + ch * 8),
+                                       (__attribute__((address_space(3))) void*)(kvs + KVB + pc * 1024),
+                                       16, 0, 0);
+    }
+  };
 
   // loop-invariant LDS read offsets (the rest are immediates)
   int rowb[2], trb[2];
@@ -165,142 +205,186 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
              8 * (tp & 1);
   }
   const int cstb = 2 * TILEB + 4 * (4 * h);
+  const int krow = wave * 32 + c;  // this lane's key within the item
 
-  x8 kf[KS], vf[KS];
-#pragma unroll
-  for (int kk = 0; kk < KS; ++kk) {
-    kf[kk] = ld8(K + (int64_t)key_c * p.k_ss + kk * 16 + 8 * h);
-    vf[kk] = ld8(V + (int64_t)key_c * p.v_ss + kk * 16 + 8 * h);
-  }
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
-  __syncthreads();  // vmcnt(0) + barrier: step 0 landed
+  // round k of workgroup w takes item k*G + (k odd ? G-1-w : w): a snake over the
+  // heaviest-first list, so every workgroup's sum of causal work is balanced
+  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  auto item_of = [&](int k) { return k * G + ((k & 1) ? G - 1 - w : w); };
+  int k = 0, it = item_of(0);
+  if (it >= nitems) return;  // whole workgroup (grid <= items; defensive)
+  Item cur;
+  decode(it, cur);
+  kv_prefetch(cur);
+  if (cur.nsteps > 0) prefetch(cur, 0, 0);
+  int gstep = 0;  // ring parity runs across items
+  __syncthreads();  // vmcnt(0) + barrier: K/V rows and step 0 landed
 
-  for (int step = 0; step < nsteps; ++step) {
-    const int hs = step / nsteps_q;
-    const int q0 = q_first + (step - hs * nsteps_q) * BQ2;
-    const int buf = step & 1;
-    if (step + 1 < nsteps) prefetch(step + 1, buf ^ 1);
-    const char* bb = lds + buf * BUFB;
-    const uint32_t trv0 = (uint32_t)(uintptr_t)(bb + trb[0]);
-    const uint32_t trv1 = (uint32_t)(uintptr_t)(bb + trb[1]);
-    static_for<BQ2 / 32>([&](auto s2c) {
-      constexpr int s2 = decltype(s2c)::value;
-      const char* qb = bb + s2 * 4 * RG;  // 32 rows = 4 row groups
-      const float* cst = reinterpret_cast<const float*>(bb + cstb) + 32 * s2;
-      const int q0s = q0 + 32 * s2;
-      f4 l24[4], nd4[4];
+  while (true) {
+    const int kbase = cur.nb * BNK + wave * 32;
+    const int key = kbase + c;
+    x8 kf[KS], vf[KS];
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        l24[rg] = *reinterpret_cast<const f4*>(cst + 8 * rg);
-        nd4[rg] = *reinterpret_cast<const f4*>(cst + BQ2 + 8 * rg);
-      }
-      // dP accumulator starts at -delta (row constant): dS = P * (dP - delta)
-      f32x16 dpacc = __builtin_shufflevector(__builtin_shufflevector(nd4[0], nd4[1], 0, 1, 2, 3, 4, 5, 6, 7),
-                                             __builtin_shufflevector(nd4[2], nd4[3], 0, 1, 2, 3, 4, 5, 6, 7),
-                                             0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-      f32x16 sacc;
+    for (int kk = 0; kk < KS; ++kk) {
+      const int so = krow * ROWB + 16 * ((2 * kk + h) ^ (krow % CH));
+      kf[kk] = *reinterpret_cast<const x8*>(kvs + so);
+      vf[kk] = *reinterpret_cast<const x8*>(kvs + KVB + so);
+    }
+    f32x16 dk[DT], dv[DT];
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int o = rowb[kk & 1] + 512 * (kk >> 1);
-        const x8 qa = *reinterpret_cast<const x8*>(qb + o);
-        const x8 da = *reinterpret_cast<const x8*>(qb + TILEB + o);
-        if (kk == 0) {
-          sacc = mfma_vgpr0<T>(qa, kf[0]);
-          mfma_vgpr<T, 1>(dpacc, da, vf[0]);
-        } else {
-          mfma_vgpr<T>(sacc, qa, kf[kk]);
-          mfma_vgpr<T>(dpacc, da, vf[kk]);
-        }
-      }
-      x4 doa[2][DT][2], qta[2][DT][2];
-      static_for<2>([&](auto sc) {
-        static_for<DT>([&](auto dc) {
-          constexpr int o = s2 * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
-          doa[sc][dc][0] = tr_read_imm<TILEB + o, T>(trv0);
-          doa[sc][dc][1] = tr_read_imm<TILEB + o, T>(trv1);
-          qta[sc][dc][0] = tr_read_imm<o, T>(trv0);
-          qta[sc][dc][1] = tr_read_imm<o, T>(trv1);
-        });
-      });
-      mfma_drain();
-      const bool need_mask = (q0s + 32 > p.sq) || (kbase + 32 > p.sk) ||
-                             (CAUSAL && (kbase + 31 > q0s + off));
+    for (int d = 0; d < DT; ++d)
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -l24[i >> 2][i & 3]));
-      if (need_mask) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qr = q0s + acc_row(i, h);
-          const bool ok = (qr < p.sq) & (key < p.sk) & (!CAUSAL | (key <= qr + off));
-          sacc[i] = ok ? sacc[i] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
-      lds_wait();  // the asm transposed reads above
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const x8 pf = acc_frag<T>(sacc, s);
-        const x8 sf = acc_frag<T>(dpacc, s);
-#pragma unroll
-        for (int d = 0; d < DT; ++d) {
-          if (d == 0) mfma_agpr<T, 1>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
-          else mfma_agpr<T>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
-          mfma_agpr<T>(dk[d], join<T>(qta[s][d][0], qta[s][d][1]), sf);
-        }
-      }
-    });
-    __syncthreads();  // vmcnt(0) + barrier: step+1 landed, this step's reads retired
-  }
+      for (int i = 0; i < 16; ++i) dk[d][i] = dv[d][i] = 0.f;
+    const int nit = item_of(k + 1);
+    const bool has_next = nit < nitems;
+    const int nsteps = cur.nsteps;
 
-  mfma_drain();
-  if (S > 1) {  // fp32 partial sums; fa_dkv_reduce_k adds the splits in order
-    if (key < p.sk) {
-      float* W = P.dkv_ws + ((((int64_t)split * p.b + b) * p.nkv + g) * p.sk + key) * 2 * HD;
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
+    for (int step = 0; step < nsteps; ++step) {
+      const int hs = step / cur.nsteps_q;
+      const int q0 = cur.q_first + (step - hs * cur.nsteps_q) * BQ2;
+      const int buf = gstep & 1;
+      if (step + 1 < nsteps) {
+        prefetch(cur, step + 1, buf ^ 1);
+      } else if (has_next) {  // (next item decoded where used: fewer live registers)
+        Item nx;
+        decode(nit, nx);
+        if (nx.nsteps > 0) prefetch(nx, 0, buf ^ 1);
+      }
+      // the staging image was read at the item start, before step 0's barrier
+      if (step == 1 && has_next) {
+        Item nx;
+        decode(nit, nx);
+        kv_prefetch(nx);
+      }
+      const char* bb = lds + buf * BUFB;
+      const uint32_t trv0 = (uint32_t)(uintptr_t)(bb + trb[0]);
+      const uint32_t trv1 = (uint32_t)(uintptr_t)(bb + trb[1]);
+      static_for<BQ2 / 32>([&](auto s2c) {
+        constexpr int s2 = decltype(s2c)::value;
+        const char* qb = bb + s2 * 4 * RG;  // 32 rows = 4 row groups
+        const float* cst = reinterpret_cast<const float*>(bb + cstb) + 32 * s2;
+        const int q0s = q0 + 32 * s2;
+        f4 l24[4], nd4[4];
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
-          f4 wk, wv;
+          l24[rg] = *reinterpret_cast<const f4*>(cst + 8 * rg);
+          nd4[rg] = *reinterpret_cast<const f4*>(cst + BQ2 + 8 * rg);
+        }
+        // dP accumulator starts at -delta (row constant): dS = P * (dP - delta)
+        f32x16 dpacc = __builtin_shufflevector(__builtin_shufflevector(nd4[0], nd4[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                               __builtin_shufflevector(nd4[2], nd4[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                               0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        f32x16 sacc;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            wk[e] = dk[d][4 * rg + e];
-            wv[e] = dv[d][4 * rg + e];
+        for (int kk = 0; kk < KS; ++kk) {
+          const int o = rowb[kk & 1] + 512 * (kk >> 1);
+          const x8 qa = *reinterpret_cast<const x8*>(qb + o);
+          const x8 da = *reinterpret_cast<const x8*>(qb + TILEB + o);
+          if (kk == 0) {
+            sacc = mfma_vgpr0<T>(qa, kf[0]);
+            mfma_vgpr<T, 1>(dpacc, da, vf[0]);
+          } else {
+            mfma_vgpr<T>(sacc, qa, kf[kk]);
+            mfma_vgpr<T>(dpacc, da, vf[kk]);
           }
-          *reinterpret_cast<f4*>(W + d * 32 + 8 * rg + 4 * h) = wk;
-          *reinterpret_cast<f4*>(W + HD + d * 32 + 8 * rg + 4 * h) = wv;
         }
+        x4 doa[2][DT][2], qta[2][DT][2];
+        static_for<2>([&](auto sc) {
+          static_for<DT>([&](auto dc) {
+            constexpr int o = s2 * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
+            doa[sc][dc][0] = tr_read_imm<TILEB + o, T>(trv0);
+            doa[sc][dc][1] = tr_read_imm<TILEB + o, T>(trv1);
+            qta[sc][dc][0] = tr_read_imm<o, T>(trv0);
+            qta[sc][dc][1] = tr_read_imm<o, T>(trv1);
+          });
+        });
+        mfma_drain();
+        const bool need_mask = (q0s + 32 > p.sq) || (kbase + 32 > p.sk) ||
+                               (CAUSAL && (kbase + 31 > q0s + off));
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -l24[i >> 2][i & 3]));
+        if (need_mask) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qr = q0s + acc_row(i, h);
+            const bool ok = (qr < p.sq) & (key < p.sk) & (!CAUSAL | (key <= qr + off));
+            sacc[i] = ok ? sacc[i] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
+        lds_wait();  // the asm transposed reads above
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const x8 pf = acc_frag<T>(sacc, s);
+          const x8 sf = acc_frag<T>(dpacc, s);
+#pragma unroll
+          for (int d = 0; d < DT; ++d) {
+            if (d == 0) mfma_agpr<T, 1>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
+            else mfma_agpr<T>(dv[d], join<T>(doa[s][d][0], doa[s][d][1]), pf);
+            mfma_agpr<T>(dk[d], join<T>(qta[s][d][0], qta[s][d][1]), sf);
+          }
+        }
+      });
+      __syncthreads();  // vmcnt(0) + barrier: next step (or item) landed, this step's reads retired
+      ++gstep;
     }
-    return;
-  }
-  if (key < p.sk) {
-    T* DK = (T*)P.dk + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg + (int64_t)key * p.k_ss;
-    T* DV = (T*)P.dv + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + (int64_t)key * p.v_ss;
-    const float *rc = nullptr, *rs = nullptr;
-    if (p.rope_cos) rope_rows<HD>(p, b, key, rc, rs);
+    // items with < 2 steps: nothing of the next item was loaded in the loop
+    if (has_next && nsteps <= 1) {
+      Item nx;
+      decode(nit, nx);
+      if (nsteps == 0 && nx.nsteps > 0) prefetch(nx, 0, gstep & 1);
+      kv_prefetch(nx);
+    }
+
+    mfma_drain();
+    if (key < p.sk) {
+      if (S > 1) {  // fp32 partial sums; fa_dkv_reduce_k adds the splits in order
+        float* W = P.dkv_ws + ((((int64_t)cur.split * p.b + cur.b) * p.nkv + cur.g) * p.sk + key) * 2 * HD;
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
+        for (int d = 0; d < DT; ++d)
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        float f[4];
+          for (int rg = 0; rg < 4; ++rg) {
+            f4 wk, wv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) f[e] = dk[d][4 * rg + e] * p.scale;
-        if (rc) rope_inv4(f, rc, rs, (d * 32 + 8 * rg + 4 * h) / 2);
-        x4 wk, wv;
+            for (int e = 0; e < 4; ++e) {
+              wk[e] = dk[d][4 * rg + e];
+              wv[e] = dv[d][4 * rg + e];
+            }
+            *reinterpret_cast<f4*>(W + d * 32 + 8 * rg + 4 * h) = wk;
+            *reinterpret_cast<f4*>(W + HD + d * 32 + 8 * rg + 4 * h) = wv;
+          }
+      } else {
+        T* DK = (T*)P.dk + (int64_t)cur.b * p.k_sb + (int64_t)cur.g * p.k_sg + (int64_t)key * p.k_ss;
+        T* DV = (T*)P.dv + (int64_t)cur.b * p.v_sb + (int64_t)cur.g * p.v_sg + (int64_t)key * p.v_ss;
+        const float *rc = nullptr, *rs = nullptr;
+        if (p.rope_cos) rope_rows<HD>(p, cur.b, key, rc, rs);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          wk[e] = (T)f[e];
-          wv[e] = (T)dv[d][4 * rg + e];
+        for (int d = 0; d < DT; ++d) {
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            float f[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f[e] = dk[d][4 * rg + e] * p.scale;
+            if (rc) rope_inv4(f, rc, rs, (d * 32 + 8 * rg + 4 * h) / 2);
+            x4 wk, wv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              wk[e] = (T)f[e];
+              wv[e] = (T)dv[d][4 * rg + e];
+            }
+            *reinterpret_cast<x4*>(DK + d * 32 + 8 * rg + 4 * h) = wk;
+            *reinterpret_cast<x4*>(DV + d * 32 + 8 * rg + 4 * h) = wv;
+          }
         }
-        *reinterpret_cast<x4*>(DK + d * 32 + 8 * rg + 4 * h) = wk;
-        *reinterpret_cast<x4*>(DV + d * 32 + 8 * rg + 4 * h) = wv;
       }
     }
+    if (!has_next) break;
+    if (nsteps <= 1) __syncthreads();  // the loads issued after the loop landed
+    ++k;
+    it = nit;
+    decode(it, cur);
   }
 }
 
@@ -527,7 +611,17 @@ void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
   const AttnParams& p = P.f;
   const int64_t rows = (int64_t)p.b * p.nq * p.sq;
   hipLaunchKernelGGL((fa_delta_k<T, HD>), dim3((rows + 255) / 256), dim3(256), 0, s, P);
-  const dim3 gkv((p.sk + BNK - 1) / BNK, p.nkv * (P.kv_split > 1 ? P.kv_split : 1), p.b);
+  // dK/dV: persistent, min(items, CUs) workgroups (EMA_FA_DKDV_GRID=full: one per item)
+  static const int ncu = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    const char* e = getenv("EMA_FA_DKDV_GRID");
+    return (e && e[0] == 'f') ? (1 << 30) : n;
+  }();
+  const long kv_items = (long)((p.sk + BNK - 1) / BNK) * p.nkv * (P.kv_split > 1 ? P.kv_split : 1) * p.b;
+  const dim3 gkv((unsigned)(kv_items < ncu ? kv_items : ncu));
   const int64_t kvred = (int64_t)p.b * p.nkv * p.sk * (2 * HD / 4);
   const int wv = flash_attn_waves(p.b, p.sq, p.nq, HD);
   const dim3 gq(((p.sq + 255) / 256) * p.nq * p.b);
