@@ -53,8 +53,10 @@ MODELS = {
 }
 
 PRESETS = {
-    # BASELINE config #2 (the headline): Llama-2-7B, pure DP (+ dist-opt at N > 1)
-    "llama7b-dp": dict(model="llama2-7b", tp=1, pp=1, seq=1024, mbs=16, nmicro=2),
+    # BASELINE config #2 (the headline): Llama-2-7B, pure DP (+ dist-opt at N > 1).
+    # 16 x 8 = 128 sequences per GPU per step: a global batch of 1024 at 8 GPUs,
+    # the reference's own P1 setting (gbs 1000 of seq 1024).
+    "llama7b-dp": dict(model="llama2-7b", tp=1, pp=1, seq=1024, mbs=16, nmicro=8),
     # config #3
     "llama7b-tp8-seq4096": dict(model="llama2-7b", tp=8, pp=1, seq=4096, mbs=4, nmicro=4,
                                 sp=True),
