@@ -126,38 +126,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
       }
   };
 
+  if (ntiles > 0) load_tile(0);
   x8 qf[KS];
-  if (p.q_lds) {
-    // Q rows by LDS-DMA (coalesced 1-KiB pieces, 16-B chunks XOR-swizzled by
-    // row) into the start of the still unused K/V ring, read back as MFMA
-    // fragments; the ring is then refilled with K/V tile 0.
-    constexpr int ROWB = HD * 2, QPW = BMW * ROWB / 1024 / WAVES;
-    static_assert(BMW * ROWB <= (int)sizeof(lds), "Q staging must fit the ring");
-    char* lq = reinterpret_cast<char*>(lds);
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
 #pragma unroll
-    for (int i = 0; i < QPW; ++i) {
-      const int pc = wave * QPW + i, o = pc * 1024 + 16 * ln;
-      const int row = o / ROWB, ch = ((o % ROWB) / 16) ^ (row % CPR);
-      int qr = mb * BMW + row;
-      qr = qr < p.sq ? qr : p.sq - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(Q + (int64_t)qr * p.q_ss + ch * 8),
-                                       (__attribute__((address_space(3))) void*)(lq + pc * 1024),
-                                       16, 0, 0);
-    }
-    if (ntiles > 0) load_tile(0);
-    __syncthreads();  // vmcnt(0) + barrier: Q landed
-    const int wr = wave * 32 + c;
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-      qf[kk] = *reinterpret_cast<const x8*>(lq + wr * ROWB + 16 * ((2 * kk + h) ^ (wr % CPR)));
-    __syncthreads();  // every wave holds its Q before the ring takes K/V tile 0
-  } else {
-    if (ntiles > 0) load_tile(0);
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
-  }
+  for (int kk = 0; kk < KS; ++kk) qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
   if (p.rope_cos) {
     const float *rc, *rs;
     rope_rows<HD>(p, b, qrow_c, rc, rs);
@@ -306,13 +278,7 @@ int flash_attn_waves(int b, int sq, int nq, int hd) {
   return (hd == 64 || blocks8 < 512) ? 4 : 8;
 }
 
-void flash_attn_fwd(const AttnParams& p0, int dt, hipStream_t s) {
-  static const int qlds = [] {  // EMA_FA_QLDS=0: per-lane Q loads (A/B)
-    const char* e = getenv("EMA_FA_QLDS");
-    return e ? atoi(e) : 1;
-  }();
-  AttnParams p = p0;
-  p.q_lds = qlds;
+void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
   const bool w4 = flash_attn_waves(p.b, p.sq, p.nq, p.hd) == 4;
   if (dt == DT_BF16) {
     if (p.hd == 128) w4 ? fa::launch_fwd2<bf16, 128, 4>(p, s) : fa::launch_fwd2<bf16, 128, 8>(p, s);

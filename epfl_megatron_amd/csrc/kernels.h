@@ -113,7 +113,6 @@ struct AttnParams {
   const float* rope_sin;
   const int64_t* rope_pos;  // [b, s] position ids (row stride rope_pos_sb) or null: row index
   int64_t rope_pos_sb;
-  int q_lds;  // forward: stage Q through LDS by LDS-DMA (set by the launcher)
 };
 struct AttnBwdParams {
   AttnParams f;
