@@ -534,9 +534,8 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   p.dq = dq.data_ptr();
   p.dk = dk.data_ptr();
   p.dv = dv.data_ptr();
-  auto delta = at::empty({3 * b * nq * sq}, q.options().dtype(at::kFloat));
-  p.delta = delta.data_ptr<float>();
-  p.ndelta = p.delta + b * nq * sq;
+  auto rowc = at::empty({2 * b * nq * sq}, q.options().dtype(at::kFloat));
+  p.ndelta = rowc.data_ptr<float>();
   p.lse2 = p.ndelta + b * nq * sq;
   p.kv_split = ema::flash_attn_kv_split((int)b, (int)sk, (int)nq, (int)nkv);
   at::Tensor ws;

@@ -1,7 +1,7 @@
 // FlashAttention-2 backward for gfx950 (MI355X), native GQA/MQA, causal.
 //
-// Two MFMA kernels after a delta = rowsum(dO * O) pre-pass; neither needs
-// atomics:
+// Two MFMA kernels, dQ first (it also produces delta = rowsum(dO * O) and
+// the LSE in log2 units for the dK/dV kernel); neither needs atomics:
 //
 // fa_bwd_dkdv2_k -- workgroup = 4 waves = 128 keys of one (batch, KV group);
 //   each wave keeps its 32 keys' K and V fragments in registers and
@@ -42,30 +42,6 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 constexpr int BNK = 128;  // keys per dK/dV workgroup
 constexpr int KT = 64;    // keys per dQ step
 
-template <typename T, int HD>
-__global__ __launch_bounds__(256) void fa_delta_k(const AttnBwdParams P) {
-  const AttnParams& p = P.f;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)p.b * p.nq * p.sq;
-  if (t >= total) return;
-  const int q = (int)(t % p.sq);
-  const int head = (int)((t / p.sq) % p.nq);
-  const int b = (int)(t / ((int64_t)p.sq * p.nq));
-  const int64_t off = (int64_t)b * p.o_sb + (int64_t)q * p.o_ss + (int64_t)head * p.o_sh;
-  const T* o = (const T*)p.o + off;
-  const T* d = (const T*)P.dout + off;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < HD; c += 8) {
-    const typename MT<T>::x8 a = ld8(o + c);
-    const typename MT<T>::x8 g = ld8(d + c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)g[e];
-  }
-  P.delta[t] = s;
-  P.ndelta[t] = -s;
-  P.lse2[t] = p.lse[t] * 1.4426950408889634f;
-}
 
 // dK/dV: 4 waves x 32 keys, K/V fragments and dK^T/dV^T accumulators
 // register-resident; each step covers 64 query rows (two 32-row sub-slices)
@@ -506,9 +482,26 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
     df[kk] = ld8(DO + (int64_t)qrow_c * p.o_ss + kk * 16 + 8 * h);
   }
+  // delta = rowsum(dO * O) for this lane's row (the row's two halves live on
+  // lanes c and c + 32); the row constants the dK/dV kernel (launched after
+  // this one) streams in are written here: no separate delta pass.
   const int64_t rb = ((int64_t)b * p.nq + head) * p.sq;
   const float lse2 = p.lse[rb + qrow_c] * 1.4426950408889634f;
-  const float dlt = P.delta[rb + qrow_c];
+  float dlt = 0.f;
+  {
+    const T* O = (const T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow_c * p.o_ss + (int64_t)head * p.o_sh;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const x8 ov = ld8(O + kk * 16 + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dlt += (float)ov[e] * (float)df[kk][e];
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (h == 0 && qrow < p.sq) {
+      P.ndelta[rb + qrow] = -dlt;
+      P.lse2[rb + qrow] = lse2;
+    }
+  }
 
   f32x16 dq[DT];
 #pragma unroll
@@ -609,8 +602,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
 template <typename T, int HD>
 void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
   const AttnParams& p = P.f;
-  const int64_t rows = (int64_t)p.b * p.nq * p.sq;
-  hipLaunchKernelGGL((fa_delta_k<T, HD>), dim3((rows + 255) / 256), dim3(256), 0, s, P);
   // dK/dV: persistent, min(items, CUs) workgroups (EMA_FA_DKDV_GRID=full: one per item)
   static const int ncu = [] {
     int dev = 0, n = 256;
@@ -628,12 +619,12 @@ void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
   const dim3 gq4(((p.sq + 127) / 128) * p.nq * p.b);
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
+    if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \
+    else hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq, dim3(512), 0, s, P);         \
     hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P);              \
     if (P.kv_split > 1)                                                                   \
       hipLaunchKernelGGL((fa_dkv_reduce_k<T, HD>), dim3((unsigned)((kvred + 255) / 256)), \
                          dim3(256), 0, s, P);                                             \
-    if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \
-    else hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq, dim3(512), 0, s, P);         \
   }
   if (p.causal) EMA_FA_BWD(true) else EMA_FA_BWD(false)
 #undef EMA_FA_BWD

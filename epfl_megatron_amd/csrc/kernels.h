@@ -120,9 +120,8 @@ struct AttnBwdParams {
   void* dq;  // same strides as q
   void* dk;  // same strides as k
   void* dv;  // same strides as v
-  float* delta;   // fp32 [b, nq, sq] workspace
-  float* ndelta;  // fp32 [b, nq, sq]: -delta (initial dP accumulator of the v2 kernels)
-  float* lse2;    // fp32 [b, nq, sq]: lse * log2(e)
+  float* ndelta;  // fp32 [b, nq, sq]: -delta, written by the dQ kernel (initial dP accumulator)
+  float* lse2;    // fp32 [b, nq, sq]: lse * log2(e), written by the dQ kernel
   float* dkv_ws;  // fp32 [kv_split][b][nkv][sk][2][hd] partial dK / dV (kv_split > 1)
   int kv_split;    // query heads of a KV group split over this many dK/dV workgroups
 };
