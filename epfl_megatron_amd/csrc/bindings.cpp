@@ -78,8 +78,17 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, do
   return {y, rstd, sum};
 }
 
+// fp32 main_grad a fused norm backward writes its parameter gradient into
+static float* grad_acc_ptr(const c10::optional<at::Tensor>& g, int64_t H, const char* what) {
+  if (!(g.has_value() && g->defined())) return nullptr;
+  TORCH_CHECK(g->scalar_type() == at::kFloat && g->is_contiguous() && g->numel() == H && g->is_cuda(),
+              what, " must be a contiguous fp32 CUDA tensor of hidden size");
+  return g->data_ptr<float>();
+}
+
 std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
+                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                                    const c10::optional<at::Tensor>& dw_acc, bool accumulate) {
   check_gpu(x, "x");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
@@ -90,17 +99,21 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   auto dr = check_res(dres, x, "dres");
   auto wc = as_dtype(w, x);
   auto dx = at::empty_like(x);
-  auto dw = at::empty({H}, x.options());
+  float* acc = grad_acc_ptr(dw_acc, H, "dw_acc");
+  auto dw = acc ? at::Tensor() : at::empty({H}, x.options());
   const int P = ema::norm_bwd_workspace_rows(rows);
   auto part = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     ema::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), rstd.data_ptr<float>(),
                      dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
-                     part.data_ptr<float>(), dw.data_ptr(), rows, H, dt, cur_stream());
+                     part.data_ptr<float>(), acc ? nullptr : dw.data_ptr(), acc,
+                     accumulate ? 1 : 0, rows, H, dt, cur_stream());
+  } else if (acc) {
+    if (!accumulate) dw_acc->zero_();
   } else {
     dw.zero_();
   }
-  return {dx, dw.to(w.scalar_type())};
+  return {dx, acc ? at::Tensor() : dw.to(w.scalar_type())};
 }
 
 std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w,
@@ -133,7 +146,10 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w,
 std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
                                       const at::Tensor& w, const at::Tensor& mean,
                                       const at::Tensor& rstd,
-                                      const c10::optional<at::Tensor>& dres) {
+                                      const c10::optional<at::Tensor>& dres,
+                                      const c10::optional<at::Tensor>& dw_acc,
+                                      const c10::optional<at::Tensor>& db_acc, bool accumulate_w,
+                                      bool accumulate_b) {
   check_gpu(x, "x");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "shape mismatch");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dtype mismatch");
@@ -144,21 +160,25 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
   auto dr = check_res(dres, x, "dres");
   auto wc = as_dtype(w, x);
   auto dx = at::empty_like(x);
-  auto dw = at::empty({H}, x.options());
-  auto db = at::empty({H}, x.options());
+  float* wacc = grad_acc_ptr(dw_acc, H, "dw_acc");
+  float* bacc = grad_acc_ptr(db_acc, H, "db_acc");
+  auto dw = wacc ? at::Tensor() : at::empty({H}, x.options());
+  auto db = bacc ? at::Tensor() : at::empty({H}, x.options());
   const int P = ema::norm_bwd_workspace_rows(rows);
   auto pw = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   auto pb = at::empty({(int64_t)P, H}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     ema::layernorm_bwd(dy.data_ptr(), x.data_ptr(), wc.data_ptr(), mean.data_ptr<float>(),
                        rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr,
-                       dx.data_ptr(), pw.data_ptr<float>(), pb.data_ptr<float>(), dw.data_ptr(),
-                       db.data_ptr(), rows, H, dt, cur_stream());
+                       dx.data_ptr(), pw.data_ptr<float>(), pb.data_ptr<float>(),
+                       wacc ? nullptr : dw.data_ptr(), bacc ? nullptr : db.data_ptr(), wacc, bacc,
+                       accumulate_w ? 1 : 0, accumulate_b ? 1 : 0, rows, H, dt, cur_stream());
   } else {
-    dw.zero_();
-    db.zero_();
+    if (wacc) { if (!accumulate_w) dw_acc->zero_(); } else dw.zero_();
+    if (bacc) { if (!accumulate_b) db_acc->zero_(); } else db.zero_();
   }
-  return {dx, dw.to(w.scalar_type()), db.to(w.scalar_type())};
+  return {dx, wacc ? at::Tensor() : dw.to(w.scalar_type()),
+          bacc ? at::Tensor() : db.to(w.scalar_type())};
 }
 
 // ---------------------------------------------------------------- rope
@@ -657,11 +677,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),
         py::arg("res") = py::none());
   m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("rstd"),
-        py::arg("dres") = py::none());
+        py::arg("dres") = py::none(), py::arg("dw_acc") = py::none(),
+        py::arg("accumulate") = false);
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"),
         py::arg("res") = py::none());
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"),
-        py::arg("mean"), py::arg("rstd"), py::arg("dres") = py::none());
+        py::arg("mean"), py::arg("rstd"), py::arg("dres") = py::none(),
+        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(),
+        py::arg("accumulate_w") = false, py::arg("accumulate_b") = false);
   m.def("rope_qkv_inplace", &rope_qkv_inplace);
   m.def("glu_fwd", &glu_fwd);
   m.def("glu_bwd", &glu_bwd);

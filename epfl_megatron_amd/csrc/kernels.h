@@ -14,17 +14,20 @@ int norm_bwd_workspace_rows(int64_t rows);  // rows of the fp32 [*, H] partial w
 int norm_max_hidden(int dtype);
 // res/sum_out (nullable): fused residual add, the norm input is x + res and
 // is also written to sum_out.  dres (nullable): added to dx in backward.
+// dw_acc / db_acc (nullable): the weight / bias gradients go into these fp32
+// buffers (the parameters' main_grad; += when accumulate) instead of dw / db.
 void rmsnorm_fwd(const void* x, const void* res, void* sum_out, const void* w, void* y,
                  float* rstd, int64_t rows, int H, float eps, int dt, hipStream_t s);
 void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
-                 const void* dres, void* dx, float* dw_part, void* dw, int64_t rows, int H,
-                 int dt, hipStream_t s);
+                 const void* dres, void* dx, float* dw_part, void* dw, float* dw_acc,
+                 int accumulate, int64_t rows, int H, int dt, hipStream_t s);
 void layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b,
                    void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
                    hipStream_t s);
 void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                    const float* rstd, const void* dres, void* dx, float* dw_part,
-                   float* db_part, void* dw, void* db, int64_t rows, int H, int dt,
+                   float* db_part, void* dw, void* db, float* dw_acc, float* db_acc,
+                   int accumulate_w, int accumulate_b, int64_t rows, int H, int dt,
                    hipStream_t s);
 
 // ---- rope.hip ----------------------------------------------------------------

@@ -476,25 +476,30 @@ __global__ __launch_bounds__(256) void colsum_stage1_k(const float* __restrict__
   }
 }
 
+// acc != nullptr: the column sums go straight into the parameter's fp32
+// main_grad (= when !accumulate, += otherwise) — no bf16 rounding of the
+// weight gradient and no separate accumulate kernel.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_stage2_k(const float* __restrict__ part2,
-                                                       T* __restrict__ out, int H) {
+                                                       T* __restrict__ out, float* __restrict__ acc,
+                                                       int accumulate, int H) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= H) return;
   float s = 0.f;
 #pragma unroll
   for (int p = 0; p < kSplits; ++p) s += part2[(int64_t)p * H + j];
-  out[j] = from_f<T>(s);
+  if (acc) acc[j] = accumulate ? acc[j] + s : s;
+  else out[j] = from_f<T>(s);
 }
 
 // part holds P + kSplits rows: [0, P) stage-1 input, [P, P + kSplits) stage-2 input.
 template <typename T>
-void colsum(float* part, T* out, int P, int H, hipStream_t s) {
+void colsum(float* part, T* out, float* acc, int accumulate, int P, int H, hipStream_t s) {
   float* part2 = part + (int64_t)P * H;
   hipLaunchKernelGGL(colsum_stage1_k, dim3((H + 63) / 64, kSplits), dim3(256), 0, s, part,
                      part2, P, H);
   hipLaunchKernelGGL((colsum_stage2_k<T>), dim3((H + 255) / 256), dim3(256), 0, s, part2, out,
-                     H);
+                     acc, accumulate, H);
 }
 
 template <typename T>
@@ -564,8 +569,8 @@ void launch_rms_bwd(const void* dy, const void* x, const void* w, const float* r
 }
 
 void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
-                 const void* dres, void* dx, float* dw_part, void* dw, int64_t rows, int H,
-                 int dt, hipStream_t s) {
+                 const void* dres, void* dx, float* dw_part, void* dw, float* dw_acc,
+                 int accumulate, int64_t rows, int H, int dt, hipStream_t s) {
   const int P = norm_bwd_partials(rows);
   const int blocks = P / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
@@ -586,7 +591,7 @@ void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd
                          (const T*)x, (const float*)nullptr, rstd, dw_part, (float*)nullptr,
                          rows, H, rpc);
     }
-    colsum<T>(dw_part, (T*)dw, P, H, s);
+    colsum<T>(dw_part, (T*)dw, dw_acc, accumulate, P, H, s);
   });
 }
 
@@ -605,7 +610,8 @@ void layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w,
 
 void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                    const float* rstd, const void* dres, void* dx, float* dw_part, float* db_part, void* dw,
-                   void* db, int64_t rows, int H, int dt, hipStream_t s) {
+                   void* db, float* dw_acc, float* db_acc, int accumulate_w, int accumulate_b,
+                   int64_t rows, int H, int dt, hipStream_t s) {
   const int P = norm_bwd_partials(rows);
   const int blocks = P / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
@@ -627,8 +633,8 @@ void layernorm_bwd(const void* dy, const void* x, const void* w, const float* me
       hipLaunchKernelGGL((norm_dw_k<T, true>), dim3(cblocks, P), dim3(256), 0, s, (const T*)dy,
                          (const T*)x, mean, rstd, dw_part, db_part, rows, H, rpc);
     }
-    colsum<T>(dw_part, (T*)dw, P, H, s);
-    colsum<T>(db_part, (T*)db, P, H, s);
+    colsum<T>(dw_part, (T*)dw, dw_acc, accumulate_w, P, H, s);
+    colsum<T>(db_part, (T*)db, db_acc, accumulate_b, P, H, s);
   });
 }
 

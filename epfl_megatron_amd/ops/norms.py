@@ -2,7 +2,11 @@
 
 GPU: one fused HIP kernel per direction (``csrc/norms.hip``): a row per
 wave64-group, vectorised 16-byte bf16 loads, fp32 statistics, and a
-two-stage deterministic reduction for the weight/bias gradients.
+two-stage deterministic reduction for the weight/bias gradients.  Under the
+framework's DDP the reduction's second stage writes (or adds) the weight and
+bias gradients straight into the parameters' fp32 ``main_grad`` — the
+gradient-accumulation fusion the linear layers use — instead of returning a
+bf16 gradient for autograd to accumulate.
 
 Numerics follow the reference:
 * RMSNorm (``megatron/model/fused_layer_norm.py:125-139``): statistics in fp32,
@@ -11,9 +15,14 @@ Numerics follow the reference:
 * LayerNorm (N6/N7, apex ``fused_layer_norm_cuda``): fp32 mean / inverse
   std, affine in fp32, one rounding to the output dtype.
 """
+import os
+
 import torch
 
 from ._ext import ext, use_native
+
+# EMA_NORM_MAIN_GRAD=0: return bf16 weight gradients to autograd instead (A/B)
+_FUSE_MAIN_GRAD = os.environ.get("EMA_NORM_MAIN_GRAD", "1") != "0"
 
 
 def rms_norm_ref(x, weight, eps):
@@ -25,6 +34,25 @@ def rms_norm_ref(x, weight, eps):
 def layer_norm_ref(x, weight, bias, eps):
     return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), weight.float(),
                                           None if bias is None else bias.float(), eps).type_as(x)
+
+
+def _main_grad_target(param, needed):
+    """(main_grad, accumulate) when ``param``'s gradient can be written by the
+    norm backward kernel straight into its fp32 DDP buffer (``main_grad``, the
+    gradient-accumulation fusion the linear layers use), else (None, False)."""
+    if not (_FUSE_MAIN_GRAD and needed) or param is None:
+        return None, False
+    mg = getattr(param, "main_grad", None)
+    if mg is None or not mg.is_cuda or mg.dtype != torch.float32 or not mg.is_contiguous():
+        return None, False
+    return mg, not getattr(param, "_mg_fresh", False)
+
+
+def _main_grad_done(param):
+    param._mg_fresh = False
+    cb = getattr(param, "_main_grad_ready", None)
+    if cb is not None:
+        cb()
 
 
 def _rows(t, h):
@@ -56,6 +84,7 @@ class _NormResidualFn(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.has_bias = bias is not None
         ctx.shape = x.shape
+        ctx.params = (weight, bias)
         s_out = s.view(x.shape) if res is not None else x
         return y.view(x.shape), s_out
 
@@ -64,15 +93,24 @@ class _NormResidualFn(torch.autograd.Function):
         h = ctx.shape[-1]
         dy2 = _rows(dy, h)
         ds2 = None if ds is None else _rows(ds, h)
+        wp, bp = ctx.params
+        wacc, wa = _main_grad_target(wp, ctx.needs_input_grad[2])
         if ctx.is_rms:
             s, weight, rstd = ctx.saved_tensors
-            dx, dw = ext().rmsnorm_bwd(dy2, s, weight, rstd, ds2)
+            dx, dw = ext().rmsnorm_bwd(dy2, s, weight, rstd, ds2, wacc, wa)
             db = None
         else:
             s, weight, mean, rstd = ctx.saved_tensors
-            dx, dw, db = ext().layernorm_bwd(dy2, s, weight, mean, rstd, ds2)
+            bacc, ba = _main_grad_target(bp, ctx.has_bias and ctx.needs_input_grad[3])
+            dx, dw, db = ext().layernorm_bwd(dy2, s, weight, mean, rstd, ds2, wacc, bacc, wa, ba)
+            if bacc is not None:
+                _main_grad_done(bp)
+                db = None
             if not ctx.has_bias:
                 db = None
+        if wacc is not None:
+            _main_grad_done(wp)
+            dw = None
         dx = dx.view(ctx.shape)
         return dx, (dx if ctx.has_res else None), dw, db, None, None
 
@@ -84,12 +122,17 @@ class _RMSNormFn(torch.autograd.Function):
         y, rstd, _ = ext().rmsnorm_fwd(x2, weight, eps)
         ctx.save_for_backward(x2, weight, rstd)
         ctx.shape = x.shape
+        ctx.wparam = weight
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight, rstd = ctx.saved_tensors
-        dx, dw = ext().rmsnorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, rstd)
+        wacc, wa = _main_grad_target(ctx.wparam, ctx.needs_input_grad[1])
+        dx, dw = ext().rmsnorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, rstd, None, wacc, wa)
+        if wacc is not None:
+            _main_grad_done(ctx.wparam)
+            dw = None
         return dx.view(ctx.shape), dw, None
 
 
@@ -101,12 +144,23 @@ class _LayerNormFn(torch.autograd.Function):
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.has_bias = bias is not None
         ctx.shape = x.shape
+        ctx.params = (weight, bias)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight, mean, rstd = ctx.saved_tensors
-        dx, dw, db = ext().layernorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, mean, rstd)
+        wp, bp = ctx.params
+        wacc, wa = _main_grad_target(wp, ctx.needs_input_grad[1])
+        bacc, ba = _main_grad_target(bp, ctx.has_bias and ctx.needs_input_grad[2])
+        dx, dw, db = ext().layernorm_bwd(_rows(dy, x2.shape[-1]), x2, weight, mean, rstd, None,
+                                         wacc, bacc, wa, ba)
+        if wacc is not None:
+            _main_grad_done(wp)
+            dw = None
+        if bacc is not None:
+            _main_grad_done(bp)
+            db = None
         return dx.view(ctx.shape), dw, (db if ctx.has_bias else None), None
 
 

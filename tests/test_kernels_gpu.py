@@ -110,6 +110,43 @@ def test_layernorm(dtype, H):
     _close(b.grad, br.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "layernorm db")
 
 
+@pytest.mark.parametrize("is_rms", [True, False])
+def test_norm_grad_into_main_grad(is_rms):
+    """DDP gradient-accumulation fusion of the norm parameters: with a fp32
+    ``main_grad`` the backward kernel writes dW (and dB) into it (fresh: =,
+    then +=), fires ``_main_grad_ready`` and returns no autograd gradient."""
+    from epfl_megatron_amd.ops.norms import norm_residual
+    torch.manual_seed(5)
+    rows, H, dt = 300, 4096, torch.bfloat16
+    w = torch.nn.Parameter((1 + 0.1 * torch.randn(H, device=DEV)).to(dt))
+    b = None if is_rms else torch.nn.Parameter((0.1 * torch.randn(H, device=DEV)).to(dt))
+    ready = []
+    for p in (w, b):
+        if p is not None:
+            p.main_grad = torch.full((H,), 123.0, device=DEV)
+            p._mg_fresh = True
+            p._main_grad_ready = (lambda q=p: ready.append(q))
+    xs = [torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True) for _ in range(2)]
+    gs = [torch.randn(rows, H, device=DEV, dtype=dt) for _ in range(2)]
+    for x, g in zip(xs, gs):  # two micro-batches: overwrite, then accumulate
+        y, _ = norm_residual(x, None, w, b, 1e-5, is_rms)
+        y.backward(g)
+    assert w.grad is None and (b is None or b.grad is None)
+    assert len(ready) == (2 if is_rms else 4)
+    wr = w.detach().float().requires_grad_()
+    br = None if is_rms else b.detach().float().requires_grad_()
+    for x, g in zip(xs, gs):
+        xr = x.detach().float()
+        if is_rms:
+            yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+        else:
+            yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+        yr.backward(g.float())
+    _close(w.main_grad, wr.grad, 0.05 * rows ** 0.5, 3e-2, "dw into main_grad")
+    if not is_rms:
+        _close(b.main_grad, br.grad, 0.05 * rows ** 0.5, 3e-2, "db into main_grad")
+
+
 @pytest.mark.parametrize("with_pos", [False, True])
 def test_rope_inplace(with_pos):
     from epfl_megatron_amd.ops.rope import rope_table, rope_qkv_inplace, apply_rope_ref
