@@ -38,6 +38,10 @@
 //     (4 or 8 tiles of the shorter output dimension) so concurrently running
 //     workgroups share operand panels in L2.
 //
+//   * Split-K over tokens when the output has fewer tiles than CUs
+//     (TP-sharded projections): fp32 partials per split, then an ordered
+//     reduce into G — deterministic, unlike float atomics.
+//
 // Shapes: N % 256 == 0, K % 256 == 0, M % 32 == 0 (checked by the host).
 #include <cstdlib>
 
@@ -114,7 +118,7 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
-        int K, int gn) {
+        int K, int gn, int msplit, float* __restrict__ ws) {
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -122,7 +126,18 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
 
   // tile order: XCD-contiguous, then 8 (n) x 4 (k) groups
   const int ntn = N / TN, ntk = K / TK, ntiles = ntn * ntk;
-  const int lin = xcd_remap(blockIdx.x, ntiles);
+  // split-K over tokens (ws != nullptr): workgroup b takes tile b % ntiles of
+  // token split b / ntiles and stores its fp32 partial to ws[split] (ACCUM is
+  // false); wgrad_split_reduce_k adds the splits in order (deterministic)
+  const int split = (int)blockIdx.x / ntiles;
+  if (ws) {
+    const int m0s = split * msplit;
+    M = min(msplit, M - m0s);
+    dy += (int64_t)m0s * N;
+    x += (int64_t)m0s * K;
+    g = ws + (int64_t)split * N * K;
+  }
+  const int lin = xcd_remap((int)blockIdx.x - split * ntiles, ntiles);
   int tn, tk;
   if (gn > 0) {  // groups of gn n-tiles x all k-tiles, n fastest
     const int grp = lin / (gn * ntk);
@@ -388,10 +403,25 @@ int tile_group(int ntn, int ntk) {
 }
 
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
-void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s) {
+void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
+            int nsplit = 1, float* ws = nullptr) {
   const int ntiles = (N / TN) * (K / TK);
-  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(ntiles), dim3(512), 0, s,
-                     (const T*)dy, (const T*)x, g, M, N, K, tile_group(N / TN, K / TK));
+  const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
+  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(ntiles * nsplit), dim3(512), 0, s,
+                     (const T*)dy, (const T*)x, g, M, N, K, tile_group(N / TN, K / TK), msplit,
+                     nsplit > 1 ? ws : nullptr);
+}
+
+// G (+)= sum over the token splits of ws[s] (fixed order), 4 floats per thread
+__global__ __launch_bounds__(256) void wgrad_split_reduce_k(const float* __restrict__ ws,
+                                                           float* __restrict__ g, int64_t nk,
+                                                           int nsplit, int accumulate) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= nk) return;
+  f32x4 acc = accumulate ? *reinterpret_cast<const f32x4*>(g + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < nsplit; ++sp)
+    acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (int64_t)sp * nk + i));
+  *reinterpret_cast<f32x4*>(g + i) = acc;
 }
 
 }  // namespace
@@ -423,9 +453,29 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
          N * K < ((int64_t)1 << 40);
 }
 
+// Token splits for shapes with fewer 256 x 256 output tiles than CUs (the
+// TP-sharded projections): enough splits for one workgroup per CU, at most 8,
+// and at least 2048 tokens (64 ring subtiles) per split.
+int wgrad_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = (N / TN) * (K / TK);
+  if (tiles >= 256) return 1;
+  int sp = (int)((256 + tiles - 1) / tiles);
+  sp = sp < 8 ? sp : 8;
+  while (sp > 1 && M / sp < 2048) --sp;
+  return sp;
+}
+
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
-                bool accumulate, int dt, hipStream_t s) {
+                bool accumulate, int dt, hipStream_t s, int nsplit, float* ws) {
   const int iM = (int)M, iN = (int)N, iK = (int)K;
+  if (nsplit > 1 && ws) {
+    if (dt == DT_BF16) launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, nsplit, ws);
+    else if (dt == DT_F16) launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, nsplit, ws);
+    const int64_t nk = N * K;
+    hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)((nk / 4 + 255) / 256)), dim3(256), 0,
+                       s, ws, g, nk, nsplit, accumulate ? 1 : 0);
+    return;
+  }
   if (dt == DT_BF16) {
     if (accumulate) launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
     else launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s);

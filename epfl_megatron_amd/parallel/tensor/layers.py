@@ -162,9 +162,10 @@ def _notify_grad_ready(param):
 # default; EMA_WGRAD=hipblaslt for the library): 1.11-1.40 PF isolated vs
 # 0.94-1.16 PF and 28.3k vs 26.7k tokens/s in the 7B step (profiles/r2_wgrad_ab.txt).
 _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hip").lower() == "hip"
-# One 256x256 output tile per workgroup and no split over tokens: below one
-# tile per CU (TP-sharded 7B/70B projections) hipBLASLt's split-K wins.
-_WGRAD_MIN_TILES = 256
+# One 256x256 output tile per workgroup; below one tile per CU (TP-sharded
+# 7B/70B projections) the kernel splits the tokens over up to 8 workgroups per
+# tile (fp32 partials + ordered reduce).  Under 32 tiles hipBLASLt is used.
+_WGRAD_MIN_TILES = int(os.environ.get("EMA_WGRAD_MIN_TILES", "32"))
 # EMA_GEMM=tuned routes all three products through ops/gemm.py (per-shape
 # solution timing).  Off by default: in the full 7B step it measured 22.4k vs
 # 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —
@@ -226,8 +227,8 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
     instead of zero-filling the buffer) makes the first contribution of a step
     a plain store (beta = 0): no fill kernel, no read of the old values.  On
     the GPU the hand-written MFMA kernel (``csrc/gemm_wgrad.hip``) is used for
-    every shape it tiles with at least one tile per CU; others go to
-    hipBLASLt through ``torch.addmm``.
+    every shape it tiles (split over tokens when it has fewer tiles than CUs);
+    others go to hipBLASLt through ``torch.addmm``.
     """
     main_grad = weight.main_grad
     accumulate = not getattr(weight, "_mg_fresh", False)

@@ -406,7 +406,7 @@ def test_flash_attention_kvcache_causal_offset():
 
 
 @pytest.mark.parametrize("M,N,K", [(32, 256, 256), (96, 512, 256), (1024, 768, 512),
-                                   (8192, 256, 512)])
+                                   (8192, 256, 512), (16384, 1536, 512), (16544, 1280, 1024)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_wgrad_gemm(M, N, K, dtype):
     """Hand-written MFMA wgrad (csrc/gemm_wgrad.hip) vs fp32 reference, beta 1 and 0."""
