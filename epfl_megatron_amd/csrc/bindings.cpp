@@ -566,6 +566,45 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 
+// ---------------------------------------------------------------- decode attention
+// q [b, 1, nq, hd] (strides qs = (sb, ss, sg, sh)), k/v caches [b, sk, nkv, hd]
+// (strides (sb, ss, sg)), out [b, 1, nq, hd] (strides (sb, ss, sh)).
+void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
+                  int64_t b, int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
+                  std::vector<int64_t> qs, std::vector<int64_t> ks, std::vector<int64_t> vs,
+                  std::vector<int64_t> os, double scale) {
+  check_gpu(q, "q");
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
+              out.scalar_type() == q.scalar_type(), "q/k/v/out dtype mismatch");
+  TORCH_CHECK(ema::flash_attn_supported((int)hd, dtype_code(q)), "decode attention supports "
+              "bf16/fp16 with head_dim 64 or 128");
+  TORCH_CHECK(nkv > 0 && nq % nkv == 0 && b > 0 && sk > 0, "bad decode shape");
+  TORCH_CHECK(q.stride(-1) == 1 && k.stride(-1) == 1 && v.stride(-1) == 1 && out.stride(-1) == 1,
+              "head_dim must be contiguous");
+  for (int64_t s : ks) TORCH_CHECK(s % 8 == 0, "k strides must keep 16-byte alignment");
+  for (const at::Tensor* t : {&q, &k, &v}) check_vec_aligned(*t, "q/k/v");
+  auto span = [](int64_t b, int64_t s, int64_t n, int64_t sb, int64_t ss, int64_t sn, int64_t hd) {
+    return (b - 1) * sb + (s - 1) * ss + (n - 1) * sn + hd;
+  };
+  TORCH_CHECK(k.storage_offset() + span(b, sk, nkv, ks[0], ks[1], ks[2], hd) <=
+              (int64_t)(k.storage().nbytes() / k.element_size()), "k strides exceed storage");
+  TORCH_CHECK(v.storage_offset() + span(b, sk, nkv, vs[0], vs[1], vs[2], hd) <=
+              (int64_t)(v.storage().nbytes() / v.element_size()), "v strides exceed storage");
+  ema::DecodeParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = out.data_ptr();
+  p.b = (int)b; p.sk = (int)sk; p.nq = (int)nq; p.nkv = (int)nkv; p.hd = (int)hd;
+  p.q_sb = qs[0]; p.q_sg = qs[2]; p.q_sh = qs[3];
+  p.k_sb = ks[0]; p.k_ss = ks[1]; p.k_sg = ks[2];
+  p.v_sb = vs[0]; p.v_ss = vs[1]; p.v_sg = vs[2];
+  p.o_sb = os[0]; p.o_sh = os[2];
+  p.scale = (float)scale;
+  const int64_t ns = ema::flash_decode_splits((int)sk);
+  auto ws = at::empty({b * nq * ns * (hd + 2)}, q.options().dtype(at::kFloat));
+  p.ws_o = ws.data_ptr<float>();
+  p.ws_ml = p.ws_o + b * nq * ns * hd;
+  ema::flash_decode(p, dtype_code(q), cur_stream());
+}
+
 // ---------------------------------------------------------------- bias-dropout-add
 at::Tensor bias_dropout_add_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& x2,
                                 const c10::optional<at::Tensor>& bias, const at::Tensor& res,
@@ -711,6 +750,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_bwd", &bias_dropout_add_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_decode", &flash_decode);
   m.def("transpose16", &transpose16);
   m.def("transpose16_supported", &transpose16_supported);
 }

@@ -146,6 +146,24 @@ inline int flash_attn_kv_split(int b, int sk, int nq, int nkv) {
 // profiles/r2c_fa_waves_ab.txt.  EMA_FA_WAVES=4|8 overrides.
 int flash_attn_waves(int b, int sq, int nq, int hd);
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s);
+
+// ---- flash_decode.hip: one query token per (batch, head) against a KV cache ----
+struct DecodeParams {
+  const void* q;  // query head j of group g at b*q_sb + g*q_sg + (j % r)*q_sh
+  const void* k;  // key i of group g at b*k_sb + i*k_ss + g*k_sg
+  const void* v;
+  void* o;  // head `head` at b*o_sb + head*o_sh
+  int b, sk, nq, nkv, hd;
+  int64_t q_sb, q_sg, q_sh;
+  int64_t k_sb, k_ss, k_sg;
+  int64_t v_sb, v_ss, v_sg;
+  int64_t o_sb, o_sh;
+  float scale;
+  float* ws_o;   // fp32 [b][nq][splits][hd] chunk partials
+  float* ws_ml;  // fp32 [b][nq][splits][2] chunk (max, sum) in log2 units
+};
+int flash_decode_splits(int sk);
+void flash_decode(const DecodeParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
 // ---- gemm_wgrad.hip ------------------------------------------------------------------------------

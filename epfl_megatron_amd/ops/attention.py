@@ -15,7 +15,8 @@ straight into a ``[s, b, ng, r+2, hd]`` gradient buffer for the QKV GEMM
 backward.
 
 ``flash_attn_func`` is the general entry (separate q/k/v, ``sq <= sk`` with
-bottom-right-aligned causal mask) used by KV-cached inference.
+bottom-right-aligned causal mask) used by KV-cached inference; single-token
+decode steps go to the split-key decode kernel (``csrc/flash_decode.hip``).
 
 CPU tensors use an exact fp32 math reference (GPU test oracle and the gloo
 plumbing path).
@@ -131,6 +132,19 @@ class _FlashQKVPackedFn(torch.autograd.Function):
         return dqkv5.view(s, b, -1), None, None, None, None, None, None, None, None
 
 
+def _flash_decode(q, k, v, scale):
+    """sq == 1 against a KV cache (generation): split-key decode kernel
+    (``csrc/flash_decode.hip``); no autograd."""
+    b, _, nq, d = q.shape
+    sk, nkv = k.shape[1], k.shape[2]
+    r = nq // nkv
+    out = torch.empty(b, 1, nq, d, dtype=q.dtype, device=q.device)
+    ext().flash_decode(q, k, v, out, b, sk, nq, nkv, d, list(_bsnd_strides(q, r)),
+                       list(_bsnd_strides(k, 1)[:3]), list(_bsnd_strides(v, 1)[:3]),
+                       [out.stride(0), out.stride(1), out.stride(2)], float(scale))
+    return out
+
+
 class _FlashFn(torch.autograd.Function):
     """Separate q ``[b, sq, nq, d]``, k/v ``[b, sk, nkv, d]``."""
 
@@ -194,5 +208,12 @@ def flash_attn_func(q, k, v, causal=True, softmax_scale=None):
     """Separate tensors ``[b, s, n, d]`` (inference / generic callers)."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if use_native(q):
+        b, sq, nq = q.shape[:3]
+        r = nq // k.shape[2]
+        if sq == 1 and (r >= 2 or nq * b < 256) and not (
+                torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)):
+            # split-key decode: GQA/MQA reads each K/V byte once; small grids
+            # spread over the chunks (profiles/r2c_decode_bench.txt)
+            return _flash_decode(q, k, v, scale)  # the last position sees every cached key
         return _FlashFn.apply(q, k, v, causal, scale)
     return attention_ref(q, k, v, causal, scale)

@@ -393,6 +393,24 @@ def test_flash_attention_qkvpacked_rope(s, b, ng, r, hd, with_pos):
     _close(x.grad.cpu(), xr.grad, 6e-2, 6e-2, "qkvpacked bwd")
 
 
+@pytest.mark.parametrize("b,sk,nq,nkv,hd", [(2, 1, 8, 8, 128), (2, 77, 8, 2, 128),
+                                              (1, 300, 71, 1, 64), (3, 1000, 64, 8, 128),
+                                              (1, 4096, 32, 32, 128), (2, 513, 12, 4, 64)])
+def test_flash_decode(b, sk, nq, nkv, hd):
+    """Single-token decode against a strided [s, b, nkv, hd] KV cache (the
+    inference layout): split-key decode kernel vs fp32 reference."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    torch.manual_seed(sk + nq)
+    kmem = torch.randn(sk + 5, b + 1, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    vmem = torch.randn(sk + 5, b + 1, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    q = torch.randn(1, b, nq, hd, device=DEV, dtype=torch.bfloat16) * 2
+    keys, vals = kmem[:sk, 1:b + 1].transpose(0, 1), vmem[:sk, 1:b + 1].transpose(0, 1)
+    with torch.no_grad():
+        o = flash_attn_func(q.transpose(0, 1), keys, vals, causal=True)
+    orf = attention_ref(q.transpose(0, 1).float(), keys.float(), vals.float(), causal=True)
+    _close(o, orf, 2e-2, 2e-2, "decode")
+
+
 def test_flash_attention_kvcache_causal_offset():
     """sq < sk (decode with cache): bottom-right aligned causal mask."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
