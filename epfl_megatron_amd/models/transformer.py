@@ -8,7 +8,7 @@ Module tree and parameter names match the reference
 ``[output_layernorm]``, ``final_layernorm``.
 
 MI355X hot path (flash attention on): RMSNorm/LayerNorm HIP kernel ->
-QKV GEMM (hipBLASLt) -> in-place RoPE + FlashAttention-2 HIP kernel reading
+QKV GEMM (hipBLASLt) -> k-only RoPE pass + FlashAttention-2 HIP kernel (Q RoPE fused) reading
 the fused ``[s, b, ng, r+2, hd]`` QKV tensor through strides (native GQA, no
 K/V expansion, no rearrange copies) -> dense GEMM -> residual -> norm ->
 fc1 GEMM -> fused GLU/GeLU HIP kernel -> fc2 GEMM -> residual.
@@ -31,7 +31,8 @@ from ..parallel import tensor as tp
 from ..ops.dropout import bias_dropout_add
 from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm
-from ..ops.rope import rope_table, apply_rope_ref
+from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
+from ..ops._ext import use_native
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func
 from ..ops.activations import glu, bias_gelu, gelu
 from ..ops.softmax import FusedScaleMaskSoftmax
@@ -274,14 +275,23 @@ class ParallelAttention(MegatronModule):
         return self.dense(ctx)
 
     def _inference_forward(self, mixed, attention_mask, ip, position_ids, rope):
+        s0 = ip.sequence_len_offset
+        b0 = ip.batch_size_offset
+        if rope is not None and use_native(mixed) and mixed.is_contiguous() and \
+                not (torch.is_grad_enabled() and mixed.requires_grad):
+            # one in-place HIP pass over q and k of the fused projection, with
+            # the true positions, BEFORE caching (fixes D1)
+            sq_, b_ = mixed.shape[:2]
+            rope_qkv_inplace(mixed.view(sq_, b_, self.num_groups_per_partition,
+                                        self.q_per_group + 2, self.hidden_size_per_attention_head),
+                             rope[0], rope[1], position_ids, offset=s0)
+            rope = None
         q, k, v = self._split_qkv(mixed)
         sq, b = q.shape[:2]
         if self.layer_number not in ip.key_value_memory_dict:
             ip.key_value_memory_dict[self.layer_number] = self._allocate_kv(
                 ip.max_sequence_len, ip.max_batch_size, mixed.device)
         kmem, vmem = ip.key_value_memory_dict[self.layer_number]
-        s0 = ip.sequence_len_offset
-        b0 = ip.batch_size_offset
         if rope is not None:
             # Rotate with the true positions BEFORE caching (fixes D1).
             q = apply_rope_ref(q, rope[0], rope[1], position_ids, offset=s0)

@@ -118,3 +118,39 @@ def _sync_free(rank, world):
 def test_train_step_has_no_host_sync():
     calls = run_dist(_sync_free, 1)[0]
     assert "cuda" not in calls, calls
+
+
+def _kv_decode(rank, world):
+    """Teacher-forced KV-cached decode (prefill + one token at a time: the
+    k/q RoPE pass with the position offset, the split-key decode kernel) vs
+    one full causal forward of the same bf16 model on the GPU."""
+    import finetune
+    init_framework(LLAMA_GQA + ["--bf16"], finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.training import get_model
+    from epfl_megatron_amd.inference.forward_step import InferenceParams
+    args = get_args()
+    model = get_model(finetune.model_provider, ModelType.encoder_or_decoder, wrap_with_ddp=False)
+    _deterministic_init(model, args)
+    m = model[0].eval()
+    torch.manual_seed(3)
+    b, plen, n = 2, 37, 12
+    tokens = torch.randint(0, 512, (b, plen + n), device="cuda")
+    pos = torch.arange(plen + n, device="cuda")[None].expand(b, -1)
+    with torch.no_grad():
+        full = m(tokens, pos, None).float()
+        ip = InferenceParams(b, plen + n)
+        outs = [m(tokens[:, :plen], pos[:, :plen], None, inference_params=ip).float()]
+        ip.sequence_len_offset += plen
+        for t in range(plen, plen + n):
+            outs.append(m(tokens[:, t:t + 1], pos[:, t:t + 1], None, inference_params=ip).float())
+            ip.sequence_len_offset += 1
+    inc = torch.cat(outs, dim=1)
+    return float((inc - full).abs().max()), float(full.abs().max())
+
+
+@pytest.mark.gpu
+def test_gpu_kv_cached_decode_matches_full_forward():
+    err, scale = run_dist(_kv_decode, 1)[0]
+    assert err < 3e-2 * max(1.0, scale), (err, scale)
