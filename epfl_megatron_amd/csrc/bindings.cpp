@@ -566,6 +566,28 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   ema::flash_attn_bwd(p, dtype_code(q), cur_stream());
 }
 
+// ---------------------------------------------------------------- skinny GEMM (decode)
+bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
+  return ema::skinny_gemm_supported(M, N, K);
+}
+
+// x [M, K] @ w[N, K]^T -> [M, N]
+at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "skinny_gemm: shapes");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "skinny_gemm: contiguous operands");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type(), "skinny_gemm: dtype mismatch");
+  const int dt = dtype_code(x);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "skinny_gemm: bf16/fp16 only");
+  const int64_t M = x.size(0), N = w.size(0), K = x.size(1);
+  TORCH_CHECK(ema::skinny_gemm_supported(M, N, K), "skinny_gemm: unsupported shape");
+  check_vec_aligned(x, "x");
+  check_vec_aligned(w, "w");
+  auto y = at::empty({M, N}, x.options());
+  ema::skinny_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, dt, cur_stream());
+  return y;
+}
+
 // ---------------------------------------------------------------- decode attention
 // q [b, 1, nq, hd] (strides qs = (sb, ss, sg, sh)), k/v caches [b, sk, nkv, hd]
 // (strides (sb, ss, sg)), out [b, 1, nq, hd] (strides (sb, ss, sh)).
@@ -751,6 +773,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_decode", &flash_decode);
+  m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_gemm_supported", &skinny_gemm_supported);
   m.def("transpose16", &transpose16);
   m.def("transpose16_supported", &transpose16_supported);
 }

@@ -178,6 +178,11 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
                          int64_t K, int mode, hipStream_t s);
 bool flash_attn_supported(int hd, int dt);
 
+// ---- skinny_gemm.hip: Y[M, N] = X[M, K] W[N, K]^T for decode batches (M <= 16) ----
+bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K);
+void skinny_gemm(const void* x, const void* w, void* y, int64_t M, int64_t N, int64_t K, int dt,
+                 hipStream_t s);
+
 // ---- transpose.hip -------------------------------------------------------------------------------
 // dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.
 bool transpose16_supported(int64_t rows, int64_t cols);

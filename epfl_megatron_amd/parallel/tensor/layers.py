@@ -334,10 +334,38 @@ class _LinearFn(torch.autograd.Function):
         return grad_input, grad_weight, grad_bias, None, None, None
 
 
+# Decode-sized inference batches (<= 16 token rows, no autograd): the weight-
+# streaming HIP GEMM (csrc/skinny_gemm.hip) instead of hipBLASLt's skinny
+# tiles (profiles/r2c_skinny_gemm.txt).  EMA_SKINNY_GEMM=0 disables it.
+_SKINNY = os.environ.get("EMA_SKINNY_GEMM", "1") != "0"
+
+
+def _skinny_linear(input_, weight, bias, sequence_parallel):
+    """Y = X W^T (+ bias) through the skinny kernel when it applies, else None."""
+    if not (_SKINNY and input_.is_cuda and not sequence_parallel and not torch.is_grad_enabled()
+            and input_.dtype in (torch.bfloat16, torch.float16) and weight.dtype == input_.dtype):
+        return None
+    k = input_.shape[-1]
+    m = input_.numel() // k
+    n = weight.shape[0]
+    if m > 16 or not weight.is_contiguous() or not ext().skinny_gemm_supported(m, n, k):
+        return None
+    if (m > 8 and n > 16384) or (m > 4 and n > 24576):  # hipBLASLt's wide tiles win there
+        return None
+    x2 = input_.reshape(m, k)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    out = ext().skinny_gemm(x2, weight).view(*input_.shape[:-1], weight.shape[0])
+    return out if bias is None else out + bias
+
+
 def linear_with_grad_accumulation_and_async_allreduce(input, weight, bias,
                                                       gradient_accumulation_fusion,
                                                       async_grad_allreduce,
                                                       sequence_parallel_enabled):
+    out = _skinny_linear(input, weight, bias, sequence_parallel_enabled)
+    if out is not None:
+        return out
     return _LinearFn.apply(input, weight, bias, gradient_accumulation_fusion,
                            async_grad_allreduce, sequence_parallel_enabled)
 
@@ -411,10 +439,13 @@ class ColumnParallelLinear(torch.nn.Module):
             input_parallel = input_
         else:
             input_parallel = copy_to_tensor_model_parallel_region(input_)
-        output_parallel = _LinearFn.apply(input_parallel, self.weight, bias,
-                                          self.gradient_accumulation_fusion,
-                                          self.async_tensor_model_parallel_allreduce,
-                                          self.sequence_parallel_enabled)
+        output_parallel = _skinny_linear(input_parallel, self.weight, bias,
+                                         self.sequence_parallel_enabled)
+        if output_parallel is None:
+            output_parallel = _LinearFn.apply(input_parallel, self.weight, bias,
+                                              self.gradient_accumulation_fusion,
+                                              self.async_tensor_model_parallel_allreduce,
+                                              self.sequence_parallel_enabled)
         if self.gather_output:
             if self.sequence_parallel_enabled:
                 raise AssertionError("gather_output is incompatible with sequence parallelism")
@@ -473,8 +504,10 @@ class RowParallelLinear(torch.nn.Module):
             if self.sequence_parallel_enabled:
                 raise AssertionError("sequence parallelism needs a parallel input")
             input_parallel = scatter_to_tensor_model_parallel_region(input_)
-        output_parallel = _LinearFn.apply(input_parallel, self.weight, None,
-                                          self.gradient_accumulation_fusion, False, False)
+        output_parallel = _skinny_linear(input_parallel, self.weight, None, False)
+        if output_parallel is None:
+            output_parallel = _LinearFn.apply(input_parallel, self.weight, None,
+                                              self.gradient_accumulation_fusion, False, False)
         if self.sequence_parallel_enabled:
             output_ = reduce_scatter_to_sequence_parallel_region(output_parallel)
         else:

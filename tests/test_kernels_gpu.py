@@ -411,6 +411,26 @@ def test_flash_decode(b, sk, nq, nkv, hd):
     _close(o, orf, 2e-2, 2e-2, "decode")
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (5, 12288, 4096), (16, 4096, 11008),
+                                   (8, 32000, 4096), (3, 1376, 512)])
+def test_skinny_gemm(M, N, K):
+    """Decode-batch weight-streaming GEMM vs fp32 reference, and the linear
+    layers' no-grad dispatch to it."""
+    C = _ext()
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    assert C.skinny_gemm_supported(M, N, K)
+    y = C.skinny_gemm(x, w)
+    _close(y, x.float() @ w.float().t(), 2e-2, 2e-2, "skinny gemm")
+    assert not C.skinny_gemm_supported(17, N, K) and not C.skinny_gemm_supported(M, N, K + 64)
+    from epfl_megatron_amd.parallel.tensor.layers import _skinny_linear
+    with torch.no_grad():
+        y2 = _skinny_linear(x.view(M, 1, K), w, None, False)
+    assert y2 is not None and torch.equal(y2.view(M, N), y)
+    assert _skinny_linear(x.view(M, 1, K), w, None, False) is None  # grad mode on: autograd path
+
+
 def test_flash_attention_kvcache_causal_offset():
     """sq < sk (decode with cache): bottom-right aligned causal mask."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
