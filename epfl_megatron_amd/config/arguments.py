@@ -217,6 +217,9 @@ FLAG_TABLE = {
         # MI355X additions: bucketed, overlapped DP reduction sized for xGMI.
         _flag("--ddp_bucket_size_mb", type=float, default=256.0,
               help="fp32 gradient bucket size (MiB) for the overlapped DP reduction"),
+        _flag("--ddp_comm_groups", type=int, default=1,
+              help="communicators over the DP ranks; DDP buckets are issued round-robin "
+                   "on them so several reduce concurrently (one RCCL stream each)"),
         _flag("--no_overlap_grad_reduce", action="store_false", dest="overlap_grad_reduce"),
         _flag("--no_overlap_param_gather", action="store_false", dest="overlap_param_gather",
               help="dist-opt: all-gather parameters synchronously at step end instead of "

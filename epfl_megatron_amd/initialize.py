@@ -98,7 +98,8 @@ def _initialize_distributed(args):
         state.initialize_model_parallel(args.tensor_model_parallel_size,
                                         args.pipeline_model_parallel_size,
                                         args.virtual_pipeline_model_parallel_size,
-                                        args.pipeline_model_parallel_split_rank)
+                                        args.pipeline_model_parallel_split_rank,
+                                        getattr(args, "ddp_comm_groups", 1))
 
 
 def _set_random_seed(seed_, data_parallel_random_init=False):

@@ -133,6 +133,9 @@ class DistributedDataParallel(torch.nn.Module):
         self.module = module
         self.dp_group = data_parallel_group if data_parallel_group is not None \
             else state.get_data_parallel_group()
+        # bucket i reduces / gathers on comm_groups[i % n] (own RCCL stream each)
+        self.comm_groups = [self.dp_group] if data_parallel_group is not None \
+            else state.get_data_parallel_comm_groups()
         self.dp_size = dist.get_world_size(self.dp_group)
         self.dp_rank = dist.get_rank(self.dp_group)
         self.overlap = overlap_grad_reduce and self.dp_size > 1
@@ -275,13 +278,13 @@ class DistributedDataParallel(torch.nn.Module):
     # ---- collectives -------------------------------------------------------
     def _launch(self, b):
         data = self.grad_buffer[b.start:b.end]
+        grp = self.comm_groups[b.index % len(self.comm_groups)]
         # RCCL averages inside the reduction (ncclAvg): no separate 1/dp pass.
         if self.use_distributed_optimizer:
             out = data[self.dp_rank * b.shard_size:(self.dp_rank + 1) * b.shard_size]
-            b.handle = comm.reduce_scatter_into(out, data, group=self.dp_group, op="avg",
-                                                async_op=True)
+            b.handle = comm.reduce_scatter_into(out, data, group=grp, op="avg", async_op=True)
         else:
-            b.handle = comm.all_reduce(data, group=self.dp_group, op="avg", async_op=True)
+            b.handle = comm.all_reduce(data, group=grp, op="avg", async_op=True)
         b.pending = -1  # launched
 
     def start_grad_sync(self):
@@ -348,8 +351,8 @@ class DistributedDataParallel(torch.nn.Module):
             full = self.param_buffer[b.start:b.end]
             mine = full[self.dp_rank * b.shard_size:(self.dp_rank + 1) * b.shard_size]
             self._ag_pos[b.index] = len(self._ag_handles)
-            self._ag_handles.append(comm.all_gather_into(full, mine, group=self.dp_group,
-                                                         async_op=True))
+            grp = self.comm_groups[b.index % len(self.comm_groups)]
+            self._ag_handles.append(comm.all_gather_into(full, mine, group=grp, async_op=True))
         if not self.overlap_param_gather:
             self.wait_param_sync()
 

@@ -32,6 +32,8 @@ class _State:
     position_embedding_ranks: List[int] = field(default_factory=list)
     pp_global_ranks: List[int] = field(default_factory=list)
     dp_global_ranks: List[int] = field(default_factory=list)
+    # extra communicators over the same DP ranks (one RCCL stream each)
+    dp_comm_groups: List[object] = field(default_factory=list)
     tp_global_ranks: List[int] = field(default_factory=list)
     virtual_pp_rank: Optional[int] = None
     virtual_pp_world_size: Optional[int] = None
@@ -63,11 +65,15 @@ def _new_group(ranks, backend=None):
 def initialize_model_parallel(tensor_model_parallel_size=1,
                               pipeline_model_parallel_size=1,
                               virtual_pipeline_model_parallel_size=None,
-                              pipeline_model_parallel_split_rank=None):
+                              pipeline_model_parallel_split_rank=None,
+                              data_parallel_comm_groups=1):
     """Create TP/DP/PP/model-parallel/embedding groups.
 
     Every rank must call ``new_group`` for every group in the same order
     (a torch.distributed requirement), so we iterate the full grid on all ranks.
+    ``data_parallel_comm_groups`` > 1 adds communicators over the same DP ranks:
+    each has its own RCCL stream, so the DDP buckets assigned round-robin to
+    them are reduced concurrently.
     """
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed must be initialized first")
@@ -92,6 +98,14 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
             g = _new_group(ranks)
             if rank in ranks:
                 _S.dp_group, _S.dp_global_ranks = g, [int(r) for r in ranks]
+    _S.dp_comm_groups = [_S.dp_group]
+    for _ in range(max(1, int(data_parallel_comm_groups)) - 1):
+        for p in range(npp):
+            for t in range(ntp):
+                ranks = grid[p, :, t]
+                g = _new_group(ranks)
+                if rank in ranks:
+                    _S.dp_comm_groups.append(g)
     # Model-parallel groups: fix dp, vary (pp, tp).
     for d in range(ndp):
         ranks = grid[:, d, :].reshape(-1)
@@ -136,6 +150,8 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
             if rank in ranks:
                 _S.position_embedding_ranks = pos
     from . import comm
+    for i, g in enumerate(_S.dp_comm_groups[1:]):
+        comm.name_group(g, f"dp{i + 1}")
     for g, name in ((_S.dp_group, "dp"), (_S.mp_group, "mp"), (_S.tp_group, "tp"),
                     (_S.pp_group, "pp"), (_S.embedding_group, "emb"),
                     (_S.position_embedding_group, "posemb")):
@@ -167,6 +183,12 @@ def get_pipeline_model_parallel_group():
 
 def get_data_parallel_group():
     return _need(_S.dp_group, "data parallel")
+
+
+def get_data_parallel_comm_groups():
+    """[the DP group, extra communicators over the same ranks...]."""
+    _need(_S.dp_group, "data parallel")
+    return list(_S.dp_comm_groups) or [_S.dp_group]
 
 
 def get_embedding_group():

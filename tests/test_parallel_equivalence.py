@@ -144,6 +144,18 @@ def test_llama_distributed_optimizer():
     _check(base, got)
 
 
+def test_llama_dp_concurrent_comm_groups():
+    """DDP buckets issued round-robin on two communicators over the same DP
+    ranks (--ddp_comm_groups 2, small buckets so there are many): all-reduce
+    and reduce-scatter / all-gather (dist-opt) paths match DP=1."""
+    argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "4",
+                         "--ddp_bucket_size_mb", "0.05"]
+    base = _losses(run_dist(_train, 1, argv, 3))
+    for extra in ([], ["--use_distributed_optimizer"]):
+        got = _losses(run_dist(_train, 2, argv + extra + ["--ddp_comm_groups", "2"], 3))
+        _check(base, got)
+
+
 def test_llama_pipeline_1f1b(llama_ref):
     got = _losses(run_dist(_train, 2, TINY_LLAMA + ["--pipeline_model_parallel_size", "2",
                                                      "--micro_batch_size", "2",
