@@ -41,6 +41,9 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 
 constexpr int BNK = 128;  // keys per dK/dV workgroup
 constexpr int KT = 64;    // keys per dQ step
+#ifndef DQ_RING
+#define DQ_RING 3  // K/V ring depth of the 8-wave dQ kernel (A/B: -DDQ_RING=2)
+#endif
 
 
 // dK/dV: 4 waves x 32 keys, K/V fragments and dK^T/dV^T accumulators
@@ -409,7 +412,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   const AttnParams& p = P.f;
   constexpr int NT = WAVES * 64, BMW = WAVES * 32;
   constexpr int KS = HD / 16, DT = HD / 32, CPR = HD / 8;
-  __shared__ __attribute__((aligned(16))) T lds[2 * 2 * KT * HD];
+  // K/V ring depth: 3 tiles (two in flight behind the one being read) for the
+  // one-block-per-CU 8-wave form; 2 for the 4-wave form (two blocks per CU)
+  constexpr int NB = WAVES == 8 ? DQ_RING : 2;
+  __shared__ __attribute__((aligned(16))) T lds[NB * 2 * KT * HD];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
@@ -475,6 +481,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     }
   };
   if (ntiles > 0) prefetch(0, 0);
+  if (NB == 3 && ntiles > 1) prefetch(1, 1);
 
   x8 qf[KS], df[KS];
 #pragma unroll
@@ -519,8 +526,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
 
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) prefetch(t + 1, buf ^ 1);
+    const int buf = t % NB;
+    // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
+    // retired before the barrier that ended tile t-1
+    if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
     const char* kl = reinterpret_cast<const char*>(lds + buf * 2 * KT * HD);
     const char* vl = kl + KT * ROWB;
     const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
@@ -573,7 +582,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
         });
       });
     }
-    __syncthreads();  // vmcnt(0) + barrier: tile t+1 landed, tile t's reads retired
+    if (NB == 3 && t + 2 < ntiles) {
+      // counted: tile t+1 landed, tile t+2's DMA (2 * PPW instructions) may fly on
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * PPW) : "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();  // vmcnt(0) + barrier: tile t+1 landed, tile t's reads retired
+    }
   }
 
   mfma_drain();
