@@ -1,19 +1,24 @@
 // FlashAttention-2 forward for gfx950 (MI355X), native GQA/MQA, causal.
 //
-// Workgroup = 8 waves = a 256-row query block of one (batch, query head); each
-// wave owns 32 query rows, two waves per SIMD share every K/V tile.  K/V tiles
-// of 64 keys stream through double-buffered LDS, register-staged: the next
-// tile's global loads are issued before the current tile's MFMAs and written
-// to the other buffer after them (CDNA guide T14), one barrier per tile.
+// Workgroup = WAVES waves = a WAVES*32-row query block of one (batch, query
+// head); each wave owns 32 query rows (8 waves: two per SIMD sharing every K/V
+// tile; 4 waves, two workgroups per CU, at head_dim 64 or on small grids).
+// K/V tiles of 64 keys arrive by LDS-DMA (global_load_lds, one 1-KiB piece per
+// wave instruction) into the image-(a) layout of the dQ kernel (8-row x 32-col
+// subtiles, XOR swizzle produced through the per-lane SOURCE address): no
+// staging registers and no ds_write pass; with 8 waves a 3-tile ring with a
+// counted vmcnt keeps the DMA two tiles ahead (profiles/r2c_fa_fwd_v5_ab.txt:
+// +1-2 % at s=1k, +4-8 % at s=4k, +13 % on TP-rank shapes over the earlier
+// register-staged kernel).  One barrier per tile.
 //
-// Per 32(q) x 64(k) step a wave runs 2 x HD/16 MFMAs for S^T = K Q^T and
-// 2 x 2 x HD/32 MFMAs for O^T += V^T P^T (v_mfma_f32_32x32x16).  S is computed
-// transposed ("swapped QK^T", guide T12) so a query row lives on one lane pair
-// (lane, lane^32): the online-softmax max/sum is 31 in-register ops + one
-// cross-half shuffle, the O rescale is a per-lane scalar, and the P
-// accumulator feeds the PV MFMA as its B operand with no LDS round trip.  V is
-// read from LDS with ds_read_b64_tr_b16 (hardware transpose, guide T10) from a
-// row-padded image (conflict-free); K uses an XOR-swizzled image (T2).
+// Per 32(q) x 64(k) step a wave runs 2 x HD/16 MFMAs for S^T = K Q^T (K read
+// by rows) and 2 x 2 x HD/32 MFMAs for O^T += V^T P^T (V^T by
+// ds_read_b64_tr_b16, hardware transpose, guide T10), v_mfma_f32_32x32x16.
+// S is computed transposed ("swapped QK^T", guide T12) so a query row lives on
+// one lane pair (lane, lane^32): the online-softmax max/sum is 31 in-register
+// ops + one cross-half shuffle, the O rescale is a per-lane scalar (skipped
+// when no lane's max moved), and the P accumulator feeds the PV MFMA as its B
+// operand with no LDS round trip.
 //
 // Query head j reads KV group j / (nq / nkv) directly (no K/V expansion).
 // Query blocks are dispatched on a flat grid, heaviest causal blocks of ALL
@@ -31,26 +36,23 @@ namespace ema {
 namespace fa {
 namespace {
 
-constexpr int BN = 64;
-constexpr int VPAD = 32;  // elements of padding per V row (64 B) -> conflict-free tr reads
 
 template <typename T, int HD, bool CAUSAL, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnParams p) {
+__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnParams p) {
   typedef typename MT<T>::x8 x8;
-  constexpr int NT = WAVES * 64;
-  constexpr int BMW = WAVES * 32;
-  constexpr int KS = HD / 16;
-  constexpr int DT = HD / 32;
-  constexpr int CPR = HD / 8;
-  constexpr int VST = HD + VPAD;
-  constexpr int KCH = (BN * CPR + NT - 1) / NT;  // chunks of K (and of V) per thread
-  constexpr int KTILE = BN * HD, VTILE = BN * VST;
-  __shared__ __attribute__((aligned(16))) T lds[2 * (KTILE + VTILE)];
+  typedef typename MT<T>::x4 x4;
+  constexpr int BMW = WAVES * 32, KT = 64;
+  constexpr int KS = HD / 16, DT = HD / 32;
+  constexpr int ROWB = HD * 2, RG = 8 * ROWB, PIECES = KT * ROWB / 1024, PPW = PIECES / WAVES;
+  constexpr int TB = KT * ROWB;  // bytes of one K (or V) tile
+  constexpr int NB = WAVES == 8 ? 3 : 2;
+  static_assert(PIECES % WAVES == 0, "pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char lds[NB * 2 * TB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nmb = (p.sq + BMW - 1) / BMW;
-  // flat grid: lin -> (query block, head, batch); heavy blocks first
   const int nhb = p.nq * p.b;
   const int lin = blockIdx.x;
   const int mb = CAUSAL ? (nmb - 1 - lin / nhb) : lin / nhb;
@@ -72,61 +74,40 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
     const int lim = mb * BMW + BMW + off;
     n_end = lim < p.sk ? lim : p.sk;
   }
-  const int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
-  // this wave's own last useful tile (causal): later tiles are fully masked
+  const int ntiles = n_end > 0 ? (n_end + KT - 1) / KT : 0;
   int wtiles = ntiles;
   if (CAUSAL) {
     const int wl = m0 + 32 + off;
-    const int wt = wl > 0 ? (wl + BN - 1) / BN : 0;
+    const int wt = wl > 0 ? (wl + KT - 1) / KT : 0;
     wtiles = wt < ntiles ? wt : ntiles;
   }
 
-  x8 kst[KCH], vst[KCH];
-  int krow[KCH];
-  bool kact[KCH];
-  int64_t koff[KCH], voff[KCH];
+  int srow[PPW], schunk[PPW];
 #pragma unroll
-  for (int i = 0; i < KCH; ++i) {
-    const int idx = tid + NT * i;
-    kact[i] = idx < BN * CPR;
-    krow[i] = (idx / CPR) % BN;
-    koff[i] = (int64_t)krow[i] * p.k_ss + (idx % CPR) * 8;
-    voff[i] = (int64_t)krow[i] * p.v_ss + (idx % CPR) * 8;
+  for (int i = 0; i < PPW; ++i) {
+    const int o = (wave * PPW + i) * 1024 + 16 * lane;
+    const int rem = o % RG, rem2 = rem % 512;
+    srow[i] = 8 * (o / RG) + rem2 / 64;
+    schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
   }
-  auto load_tile = [&](int n0) {
-    const T* kt = K + (int64_t)n0 * p.k_ss;
-    const T* vt = V + (int64_t)n0 * p.v_ss;
-    if (n0 + BN <= p.sk) {
+  auto prefetch = [&](int t, int slot) {
+    char* kl = lds + slot * 2 * TB;
 #pragma unroll
-      for (int i = 0; i < KCH; ++i)
-        if (kact[i]) {
-          kst[i] = ld8(kt + koff[i]);
-          vst[i] = ld8(vt + voff[i]);
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < KCH; ++i)
-        if (kact[i]) {
-          const int64_t back = (n0 + krow[i] < p.sk) ? 0 : (int64_t)(n0 + krow[i] - (p.sk - 1));
-          kst[i] = ld8(kt + koff[i] - back * p.k_ss);
-          vst[i] = ld8(vt + voff[i] - back * p.v_ss);
-        }
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;
+      int kr = t * KT + srow[i];
+      kr = kr < p.sk ? kr : p.sk - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(K + (int64_t)kr * p.k_ss + schunk[i] * 8),
+                                       (__attribute__((address_space(3))) void*)(kl + pc * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(V + (int64_t)kr * p.v_ss + schunk[i] * 8),
+                                       (__attribute__((address_space(3))) void*)(kl + TB + pc * 1024),
+                                       16, 0, 0);
     }
   };
-  auto store_tile = [&](int buf) {
-    T* kl = lds + buf * (KTILE + VTILE);
-    T* vl = kl + KTILE;
-#pragma unroll
-    for (int i = 0; i < KCH; ++i)
-      if (kact[i]) {
-        const int idx = tid + NT * i;
-        const int row = idx / CPR, ch = idx % CPR;
-        *reinterpret_cast<x8*>(kl + sw_off<HD>(row, ch * 8)) = kst[i];
-        *reinterpret_cast<x8*>(vl + row * VST + ch * 8) = vst[i];
-      }
-  };
+  if (ntiles > 0) prefetch(0, 0);
+  if (NB == 3 && ntiles > 1) prefetch(1, 1);
 
-  if (ntiles > 0) load_tile(0);
   x8 qf[KS];
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) qf[kk] = ld8(Q + (int64_t)qrow_c * p.q_ss + kk * 16 + 8 * h);
@@ -149,29 +130,49 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
   float m_i = -INFINITY, l_i = 0.f;
   const float sl2 = p.scale * 1.4426950408889634f;
 
-  if (ntiles > 0) store_tile(0);
-  __syncthreads();
+  int rowb[2], trb[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    rowb[x] = RG * (c >> 3) + 64 * (c & 7) + 16 * ((2 * x + h) ^ ((c >> 2) & 3));
+    trb[x] = RG * x + 64 * (4 * h + tq) + 16 * ((2 * ((lane >> 4) & 1) + (tp >> 1)) ^ ((h + 2 * x) & 3)) +
+             8 * (tp & 1);
+  }
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 (and 1) landed
 
-  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   for (int t = 0; t < ntiles; ++t) {
-    const int n0 = t * BN;
-    const int cur = t & 1;
-    if (t + 1 < ntiles) load_tile(n0 + BN);
-    const T* kl = lds + cur * (KTILE + VTILE);
-    const T* vl = kl + KTILE;
-
+    // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
+    // retired before the barrier that ended tile t-1
+    if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
     if (t < wtiles) {
+      const int n0 = t * KT;
+      const char* kl = lds + (t % NB) * 2 * TB;
+      const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
+      const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
       f32x16 s0, s1;
 #pragma unroll
       for (int i = 0; i < 16; ++i) s0[i] = s1[i] = 0.f;
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        const x8 ka0 = *reinterpret_cast<const x8*>(kl + sw_off<HD>(c, kk * 16 + 8 * h));
-        const x8 ka1 = *reinterpret_cast<const x8*>(kl + sw_off<HD>(32 + c, kk * 16 + 8 * h));
+        const int ko = rowb[kk & 1] + 512 * (kk >> 1);
+        const x8 ka0 = *reinterpret_cast<const x8*>(kl + ko);
+        const x8 ka1 = *reinterpret_cast<const x8*>(kl + 4 * RG + ko);
         s0 = MT<T>::mfma(ka0, qf[kk], s0);
         s1 = MT<T>::mfma(ka1, qf[kk], s1);
       }
-      const bool need_mask = CAUSAL ? (n0 + BN - 1 > m0 + off) : (n0 + BN > p.sk);
+      // V^T fragments of the tile (asm transposed reads: no wait on the DMA
+      // in flight; retired by lds_wait before the first PV MFMA)
+      x4 vf[2][2][DT][2];
+      static_for<2>([&](auto subc) {
+        static_for<2>([&](auto scc) {
+          static_for<DT>([&](auto dcc) {
+            constexpr int vo = TB + decltype(subc)::value * 4 * RG + decltype(scc)::value * 2 * RG +
+                               512 * decltype(dcc)::value;
+            vf[subc][scc][dcc][0] = tr_read_imm<vo, T>(trv0);
+            vf[subc][scc][dcc][1] = tr_read_imm<vo, T>(trv1);
+          });
+        });
+      });
+      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off) : (n0 + KT > p.sk);
       if (need_mask) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -201,9 +202,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
         rs0 += s0[i];
         rs1 += s1[i];
       }
-      float rs = rs0 + rs1;
-      rs += __shfl_xor(rs, 32, 64);
-      l_i = l_i * alpha + rs;
+      float rsum = rs0 + rs1;
+      rsum += __shfl_xor(rsum, 32, 64);
+      l_i = l_i * alpha + rsum;
       m_i = m_new;
       if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
@@ -211,24 +212,24 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
       }
+      lds_wait();
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
+      for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const x8 pf = acc_frag<T>(sub == 0 ? s0 : s1, s);
-          const int kr = sub * 32 + 16 * s + 4 * h + tq;
+        for (int sc = 0; sc < 2; ++sc) {
+          const x8 pf = acc_frag<T>(sub == 0 ? s0 : s1, sc);
 #pragma unroll
-          for (int d = 0; d < DT; ++d) {
-            const int col = d * 32 + (lane & 16) + 4 * tp;
-            const typename MT<T>::x4 va = MT<T>::tr_read(vl + kr * VST + col);
-            const typename MT<T>::x4 vb = MT<T>::tr_read(vl + (kr + 8) * VST + col);
-            o[d] = MT<T>::mfma(join<T>(va, vb), pf, o[d]);
-          }
+          for (int dc = 0; dc < DT; ++dc)
+            o[dc] = MT<T>::mfma(join<T>(vf[sub][sc][dc][0], vf[sub][sc][dc][1]), pf, o[dc]);
         }
-      }
     }
-    if (t + 1 < ntiles) store_tile(cur ^ 1);
-    __syncthreads();
+    if (NB == 3 && t + 2 < ntiles) {
+      // counted: tile t+1 landed, tile t+2's DMA (2 * PPW instructions) may fly on
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * PPW) : "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();  // vmcnt(0) + barrier: tile t+1 landed, tile t's reads retired
+    }
   }
 
   if (qrow < p.sq) {
@@ -238,10 +239,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
     for (int d = 0; d < DT; ++d) {
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        typename MT<T>::x4 w;
+        x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = (T)(o[d][4 * rg + e] * inv);
-        *reinterpret_cast<typename MT<T>::x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
+        *reinterpret_cast<x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
       }
     }
     if (h == 0) {
@@ -252,13 +253,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd2_k(const AttnPar
 }
 
 template <typename T, int HD, int WAVES>
-void launch_fwd2(const AttnParams& p, hipStream_t s) {
+void launch_fwd(const AttnParams& p, hipStream_t s) {
   const int bmw = 32 * WAVES;
   dim3 grid(((p.sq + bmw - 1) / bmw) * p.nq * p.b);
   if (p.causal)
-    hipLaunchKernelGGL((fa_fwd2_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
   else
-    hipLaunchKernelGGL((fa_fwd2_k<T, HD, false, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, false, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
 }
 
 }  // namespace
@@ -281,11 +282,11 @@ int flash_attn_waves(int b, int sq, int nq, int hd) {
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
   const bool w4 = flash_attn_waves(p.b, p.sq, p.nq, p.hd) == 4;
   if (dt == DT_BF16) {
-    if (p.hd == 128) w4 ? fa::launch_fwd2<bf16, 128, 4>(p, s) : fa::launch_fwd2<bf16, 128, 8>(p, s);
-    else w4 ? fa::launch_fwd2<bf16, 64, 4>(p, s) : fa::launch_fwd2<bf16, 64, 8>(p, s);
+    if (p.hd == 128) w4 ? fa::launch_fwd<bf16, 128, 4>(p, s) : fa::launch_fwd<bf16, 128, 8>(p, s);
+    else w4 ? fa::launch_fwd<bf16, 64, 4>(p, s) : fa::launch_fwd<bf16, 64, 8>(p, s);
   } else {
-    if (p.hd == 128) w4 ? fa::launch_fwd2<fp16, 128, 4>(p, s) : fa::launch_fwd2<fp16, 128, 8>(p, s);
-    else w4 ? fa::launch_fwd2<fp16, 64, 4>(p, s) : fa::launch_fwd2<fp16, 64, 8>(p, s);
+    if (p.hd == 128) w4 ? fa::launch_fwd<fp16, 128, 4>(p, s) : fa::launch_fwd<fp16, 128, 8>(p, s);
+    else w4 ? fa::launch_fwd<fp16, 64, 4>(p, s) : fa::launch_fwd<fp16, 64, 8>(p, s);
   }
 }
 
