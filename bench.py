@@ -40,6 +40,7 @@ import sys
 import time
 
 REF_TOKENS_PER_SEC_PER_GPU = 890.0  # BASELINE.md P1' (8x A100, seq 1024)
+BASELINE_METRIC = "tokens/sec/GPU + MFU, Llama-2 7B bf16 TP/PP/DP at 1/2/4/8 MI355X"  # BASELINE.json
 
 MODELS = {
     "llama2-7b": dict(family="llama2", L=32, h=4096, nh=32, nkv=None, ffn=11008, vocab=32000),
@@ -349,8 +350,8 @@ def main(argv=None):
                       f"per-rank tokens/s")
             label = f"{label} [{a.proxy} per-rank proxy]"
         else:
-            metric = (f"{label} bf16 training throughput, tokens/s aggregate over GPUs "
-                      "(BASELINE metric: tokens/sec/GPU + MFU; per-GPU = value / n_gpus)")
+            metric = (f"{BASELINE_METRIC} [{label} bf16 training; value = tokens/s aggregate "
+                      "over all GPUs, per-GPU = value / n_gpus, MFU in 'mfu']")
         rec = {
             "metric": metric,
             "value": round(tok_s, 1),
