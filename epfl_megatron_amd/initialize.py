@@ -75,8 +75,13 @@ def _initialize_distributed(args):
         local_rank = int(os.environ.get("LOCAL_RANK", args.rank % max(torch.cuda.device_count(), 1)))
         if args.local_rank is not None and args.local_rank != local_rank:
             local_rank = args.local_rank
-        # modulo: a rehearsal with more ranks than visible GPUs shares devices
-        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+        ndev = torch.cuda.device_count()
+        if local_rank >= ndev:
+            # one process per GPU: RCCL refuses two ranks on one device
+            # (profiles/r2c_rccl_probe_1gpu.txt), so fail with the real cause
+            raise RuntimeError(f"LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible: "
+                               "launch at most one rank per GPU")
+        torch.cuda.set_device(local_rank)
         args.local_rank = local_rank
     backend = args.distributed_backend if use_gpu else "gloo"
     args.distributed_backend = backend
