@@ -691,16 +691,20 @@ void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool ac
   TORCH_CHECK(ema::wgrad_supported(M, N, K), "wgrad_gemm: unsupported shape");
   const int dt = dtype_code(dy);
   TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "wgrad_gemm: bf16/fp16 only");
-  // split-K over tokens for shapes with fewer output tiles than CUs (fp32
-  // partials from the caching allocator, ordered reduce)
-  const int nsplit = ema::wgrad_splits(M, N, K);
+  // split-K over tokens where whole tiles leave CUs idle (fp32 partials from
+  // the caching allocator, ordered reduce)
+  const int64_t wsf = ema::wgrad_workspace_floats(M, N, K);
   at::Tensor ws;
-  if (nsplit > 1) ws = at::empty({(int64_t)nsplit * N * K}, g.options());
+  if (wsf > 0) ws = at::empty({wsf}, g.options());
   ema::wgrad_gemm(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), M, N, K, accumulate, dt,
-                  cur_stream(), nsplit, nsplit > 1 ? ws.data_ptr<float>() : nullptr);
+                  cur_stream(), wsf > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
-int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) { return ema::wgrad_splits(M, N, K); }
+// (main_tiles, tail_lin0, tail_tiles, nsplit) of a wgrad shape
+std::vector<int64_t> wgrad_plan(int64_t M, int64_t N, int64_t K) {
+  const ema::WgradPlan p = ema::wgrad_plan(M, N, K);
+  return {p.main_tiles, p.tail_lin0, p.tail_tiles, p.nsplit};
+}
 
 void wgrad_gemm_ablation(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, int64_t mode) {
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "ablation builds are bf16 only");
@@ -741,7 +745,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_gemm", &wgrad_gemm);
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
-  m.def("wgrad_splits", &wgrad_splits);
+  m.def("wgrad_plan", &wgrad_plan);
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),
         py::arg("res") = py::none());

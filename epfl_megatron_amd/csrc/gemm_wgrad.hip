@@ -38,9 +38,9 @@
 //     (4 or 8 tiles of the shorter output dimension) so concurrently running
 //     workgroups share operand panels in L2.
 //
-//   * Split-K over tokens when the output has fewer tiles than CUs
-//     (TP-sharded projections): fp32 partials per split, then an ordered
-//     reduce into G — deterministic, unlike float atomics.
+//   * Split-K over tokens where whole tiles leave CUs idle (fewer tiles than
+//     CUs, or a partial last round of tiles: wgrad_plan): fp32 partials per
+//     split, then an ordered reduce into G — deterministic, unlike atomics.
 //
 // Shapes: N % 256 == 0, K % 256 == 0, M % 32 == 0 (checked by the host).
 #include <cstdlib>
@@ -108,6 +108,27 @@ __device__ __forceinline__ void wait_subtiles(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Grouped tile order: lin -> (tn, tk).  gn > 0: groups of gn n-tiles x all
+// k-tiles, n fastest; gn < 0: groups of -gn k-tiles x all n-tiles, k fastest.
+__device__ __forceinline__ void tile_of(int lin, int ntn, int ntk, int gn, int& tn, int& tk) {
+  if (gn > 0) {
+    const int grp = lin / (gn * ntk);
+    const int first_n = grp * gn;
+    const int gsize = min(gn, ntn - first_n);
+    const int in_grp = lin - grp * gn * ntk;
+    tn = first_n + in_grp % gsize;
+    tk = in_grp / gsize;
+  } else {
+    const int gk = -gn;
+    const int grp = lin / (gk * ntn);
+    const int first_k = grp * gk;
+    const int gsize = min(gk, ntk - first_k);
+    const int in_grp = lin - grp * gk * ntn;
+    tk = first_k + in_grp % gsize;
+    tn = in_grp / gsize;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::MT<T>::x8 b,
                                         f32x4 c) {
@@ -118,44 +139,35 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
-        int K, int gn, int msplit, float* __restrict__ ws) {
+        int K, int gn, int msplit, float* __restrict__ ws, int lin0, int nlin) {
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave >> 2, wk = wave & 3;  // wn is also the ping-pong group
 
   // tile order: XCD-contiguous, then 8 (n) x 4 (k) groups
-  const int ntn = N / TN, ntk = K / TK, ntiles = ntn * ntk;
-  // split-K over tokens (ws != nullptr): workgroup b takes tile b % ntiles of
-  // token split b / ntiles and stores its fp32 partial to ws[split] (ACCUM is
-  // false); wgrad_split_reduce_k adds the splits in order (deterministic)
-  const int split = (int)blockIdx.x / ntiles;
+  const int ntn = N / TN, ntk = K / TK;
+  // This launch covers tiles [lin0, lin0 + nlin) of the grouped tile order.
+  // Split-K over tokens (ws != nullptr): workgroup b takes tile b % nlin of
+  // token split b / nlin and stores its fp32 partial as a dense 256 x 256
+  // block ws[split][tile] (ACCUM is false); wgrad_split_reduce_k adds the
+  // splits in order (deterministic)
+  const int split = (int)blockIdx.x / nlin;
+  const int lin = lin0 + xcd_remap((int)blockIdx.x - split * nlin, nlin);
+  int tn, tk;
+  tile_of(lin, ntn, ntk, gn, tn, tk);
+  int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
+  int ldg = K;  // row stride of the output
   if (ws) {
     const int m0s = split * msplit;
     M = min(msplit, M - m0s);
     dy += (int64_t)m0s * N;
     x += (int64_t)m0s * K;
-    g = ws + (int64_t)split * N * K;
+    g = ws + ((int64_t)split * nlin + (lin - lin0)) * (TN * TK);
+    ldg = TK;
   }
-  const int lin = xcd_remap((int)blockIdx.x - split * ntiles, ntiles);
-  int tn, tk;
-  if (gn > 0) {  // groups of gn n-tiles x all k-tiles, n fastest
-    const int grp = lin / (gn * ntk);
-    const int first_n = grp * gn;
-    const int gsize = min(gn, ntn - first_n);
-    const int in_grp = lin - grp * gn * ntk;
-    tn = first_n + in_grp % gsize;
-    tk = in_grp / gsize;
-  } else {       // groups of -gn k-tiles x all n-tiles, k fastest
-    const int gk = -gn;
-    const int grp = lin / (gk * ntn);
-    const int first_k = grp * gk;
-    const int gsize = min(gk, ntk - first_k);
-    const int in_grp = lin - grp * gk * ntn;
-    tk = first_k + in_grp % gsize;
-    tn = in_grp / gsize;
-  }
-  const int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
+  // operand panels: rows n0.. of dY^T, k0.. of X^T; output block origin (on, ok)
+  const int64_t on = ws ? 0 : n0, ok = ws ? 0 : k0;
 
   f32x4 acc[FA_][FB_];
 #pragma unroll
@@ -370,19 +382,19 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       const int lr = gq + 4 * k, c = 4 * cl;
       v[k] = *reinterpret_cast<const f32x4*>(reg + lr * 64 + (c ^ (16 * ((lr >> 2) & 3))));
     }
-    float* gb = g + (n0 + wn * 128 + 64 * h + gq) * (int64_t)K + k0 + wk * 64 + 4 * cl;
+    float* gb = g + (on + wn * 128 + 64 * h + gq) * (int64_t)ldg + ok + wk * 64 + 4 * cl;
     if (ACCUM) {
       f32x4 o[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k)
-        o[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(gb + (int64_t)(4 * k) * K));
+        o[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(gb + (int64_t)(4 * k) * ldg));
 #pragma unroll
       for (int k = 0; k < 16; ++k)
-        __builtin_nontemporal_store(o[k] + v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * K));
+        __builtin_nontemporal_store(o[k] + v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
     } else {
 #pragma unroll
       for (int k = 0; k < 16; ++k)
-        __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * K));
+        __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before reuse
   }
@@ -404,24 +416,32 @@ int tile_group(int ntn, int ntk) {
 
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
-            int nsplit = 1, float* ws = nullptr) {
+            int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1) {
   const int ntiles = (N / TN) * (K / TK);
+  if (nlin < 0) nlin = ntiles;
   const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
-  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(ntiles * nsplit), dim3(512), 0, s,
+  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(nlin * nsplit), dim3(512), 0, s,
                      (const T*)dy, (const T*)x, g, M, N, K, tile_group(N / TN, K / TK), msplit,
-                     nsplit > 1 ? ws : nullptr);
+                     nsplit > 1 ? ws : nullptr, lin0, nlin);
 }
 
-// G (+)= sum over the token splits of ws[s] (fixed order), 4 floats per thread
+// G[tile] (+)= sum over the token splits of ws[split][tile] (fixed order) for
+// tiles [lin0, lin0 + nlin); 64 workgroups x 256 threads x 4 floats per tile
 __global__ __launch_bounds__(256) void wgrad_split_reduce_k(const float* __restrict__ ws,
-                                                           float* __restrict__ g, int64_t nk,
-                                                           int nsplit, int accumulate) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= nk) return;
-  f32x4 acc = accumulate ? *reinterpret_cast<const f32x4*>(g + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+                                                           float* __restrict__ g, int N, int K,
+                                                           int gn, int lin0, int nlin, int nsplit,
+                                                           int accumulate) {
+  const int t = blockIdx.x / 64, part = blockIdx.x % 64;
+  int tn, tk;
+  tile_of(lin0 + t, N / TN, K / TK, gn, tn, tk);
+  const int e = (part * 256 + threadIdx.x) * 4;  // element of the 256 x 256 block
+  const int row = e / TK, col = e % TK;
+  float* gp = g + ((int64_t)tn * TN + row) * K + (int64_t)tk * TK + col;
+  f32x4 acc = accumulate ? *reinterpret_cast<const f32x4*>(gp) : f32x4{0.f, 0.f, 0.f, 0.f};
   for (int sp = 0; sp < nsplit; ++sp)
-    acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (int64_t)sp * nk + i));
-  *reinterpret_cast<f32x4*>(g + i) = acc;
+    acc += __builtin_nontemporal_load(
+        reinterpret_cast<const f32x4*>(ws + ((int64_t)sp * nlin + t) * (TN * TK) + e));
+  *reinterpret_cast<f32x4*>(gp) = acc;
 }
 
 }  // namespace
@@ -453,35 +473,70 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
          N * K < ((int64_t)1 << 40);
 }
 
-// Token splits for shapes with fewer 256 x 256 output tiles than CUs (the
-// TP-sharded projections): enough splits for one workgroup per CU, at most 8,
-// and at least 2048 tokens (64 ring subtiles) per split.
-int wgrad_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = (N / TN) * (K / TK);
-  if (tiles >= 256) return 1;
-  int sp = (int)((256 + tiles - 1) / tiles);
-  sp = sp < 8 ? sp : 8;
-  while (sp > 1 && M / sp < 2048) --sp;
-  return sp;
+// Split planning (wgrad_plan).  One workgroup owns a 256 x 256 output tile,
+// so a grid that is not a multiple of the 256 CUs ends in a partial round.
+//   * fewer tiles than CUs (TP-sharded projections): split every tile's
+//     tokens over up to 8 workgroups;
+//   * a partial last round of at most 128 tiles (e.g. the 7B fc1 wgrad:
+//     1376 tiles = 5 rounds + 96): the full rounds run unsplit and only the
+//     tail tiles are split over the idle CUs.
+// At least 2048 tokens (64 ring subtiles) per split.
+WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K) {
+  const int tiles = (int)((N / TN) * (K / TK));
+  WgradPlan pl{tiles, tiles, 0, 1};
+  auto splits_for = [&](int t) {
+    int sp = (256 + t - 1) / t;
+    sp = sp < 8 ? sp : 8;
+    while (sp > 1 && M / sp < 2048) --sp;
+    return sp;
+  };
+  if (tiles < 256) {
+    const int sp = splits_for(tiles);
+    if (sp > 1) pl = WgradPlan{0, 0, tiles, sp};
+  } else {
+    static const bool tail_split = [] {  // EMA_WGRAD_TAIL=0: no tail split (A/B)
+      const char* e = getenv("EMA_WGRAD_TAIL");
+      return !(e && e[0] == '0');
+    }();
+    const int tail = tiles % 256;
+    if (tail_split && tail > 0 && tail <= 128) {
+      int sp = 256 / tail;
+      sp = sp < 8 ? sp : 8;
+      while (sp > 1 && M / sp < 2048) --sp;
+      if (sp > 1) pl = WgradPlan{tiles - tail, tiles - tail, tail, sp};
+    }
+  }
+  return pl;
+}
+
+int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
+  const WgradPlan pl = wgrad_plan(M, N, K);
+  return pl.nsplit > 1 ? (int64_t)pl.nsplit * pl.tail_tiles * TN * TK : 0;
 }
 
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
-                bool accumulate, int dt, hipStream_t s, int nsplit, float* ws) {
+                bool accumulate, int dt, hipStream_t s, float* ws) {
   const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (nsplit > 1 && ws) {
-    if (dt == DT_BF16) launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, nsplit, ws);
-    else if (dt == DT_F16) launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, nsplit, ws);
-    const int64_t nk = N * K;
-    hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)((nk / 4 + 255) / 256)), dim3(256), 0,
-                       s, ws, g, nk, nsplit, accumulate ? 1 : 0);
-    return;
+  const WgradPlan pl = wgrad_plan(M, N, K);
+  const bool split = pl.nsplit > 1 && ws != nullptr;
+  const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
+  if (main_tiles > 0) {
+    if (dt == DT_BF16) {
+      if (accumulate) launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+    } else if (dt == DT_F16) {
+      if (accumulate) launch<fp16, true, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+    }
   }
-  if (dt == DT_BF16) {
-    if (accumulate) launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
-    else launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s);
-  } else if (dt == DT_F16) {
-    if (accumulate) launch<fp16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
-    else launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s);
+  if (split) {
+    if (dt == DT_BF16)
+      launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+    else if (dt == DT_F16)
+      launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+    hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
+                       ws, g, iN, iK, tile_group(iN / TN, iK / TK), pl.tail_lin0, pl.tail_tiles,
+                       pl.nsplit, accumulate ? 1 : 0);
   }
 }
 

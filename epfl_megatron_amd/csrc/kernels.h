@@ -168,12 +168,17 @@ void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
 // ---- gemm_wgrad.hip ------------------------------------------------------------------------------
 // G[N,K] (+)= dY[M,N]^T X[M,K]; dY/X bf16|fp16 row-major, G fp32 row-major.
-// nsplit > 1 (ws: nsplit * N * K fp32 workspace): split-K over tokens, see
-// wgrad_splits() for the split count of a shape.
+// Split-K plan of a shape: tiles [0, main_tiles) run unsplit, tiles
+// [tail_lin0, tail_lin0 + tail_tiles) split over nsplit token ranges (fp32
+// workspace of wgrad_workspace_floats() floats; none needed when nsplit == 1).
+struct WgradPlan {
+  int main_tiles, tail_lin0, tail_tiles, nsplit;
+};
 bool wgrad_supported(int64_t M, int64_t N, int64_t K);
-int wgrad_splits(int64_t M, int64_t N, int64_t K);
+WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K);
+int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
-                bool accumulate, int dt, hipStream_t s, int nsplit = 1, float* ws = nullptr);
+                bool accumulate, int dt, hipStream_t s, float* ws = nullptr);
 void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
                          int64_t K, int mode, hipStream_t s);
 bool flash_attn_supported(int hd, int dt);

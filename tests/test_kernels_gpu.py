@@ -444,7 +444,8 @@ def test_flash_attention_kvcache_causal_offset():
 
 
 @pytest.mark.parametrize("M,N,K", [(32, 256, 256), (96, 512, 256), (1024, 768, 512),
-                                   (8192, 256, 512), (16384, 1536, 512), (16544, 1280, 1024)])
+                                   (8192, 256, 512), (16384, 1536, 512), (16544, 1280, 1024),
+                                   (16384, 4352, 4096)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_wgrad_gemm(M, N, K, dtype):
     """Hand-written MFMA wgrad (csrc/gemm_wgrad.hip) vs fp32 reference, beta 1 and 0."""
@@ -461,6 +462,17 @@ def test_wgrad_gemm(M, N, K, dtype):
     C.wgrad_gemm(dy, x, g2, False)
     _close(g2, dy.float().t() @ x.float(), atol=1e-3 * math.sqrt(M), msg="store")
     assert not C.wgrad_supported(M, N + 128, K)
+
+
+def test_wgrad_plan():
+    """Split-K planning: small grids split every tile, a partial last round of
+    <= 128 tiles splits only the tail (7B fc1: 1376 tiles = 5 rounds + 96)."""
+    C = _ext()
+    assert list(C.wgrad_plan(16384, 22016, 4096)) == [1280, 1280, 96, 2]
+    assert list(C.wgrad_plan(16384, 12288, 4096)) == [768, 768, 0, 1]  # 3 full rounds
+    assert list(C.wgrad_plan(16384, 4352, 4096)) == [256, 256, 16, 8]
+    assert list(C.wgrad_plan(16384, 1536, 512)) == [0, 0, 12, 8]
+    assert list(C.wgrad_plan(1024, 768, 512)) == [6, 6, 0, 1]  # too few tokens to split
 
 
 def test_lt_gemm_layouts():
