@@ -25,11 +25,15 @@
 //     differ by instruction immediates: 4 base VGPRs per operand.
 //   * Ping-pong: waves 4..7 run one barrier behind waves 0..3 (two barriers
 //     per phase), so on every SIMD one wave's 32 MFMAs (s_setprio 1) overlap
-//     the other wave's fragment reads.  The DMA of subtile p+3 is issued from
-//     inside the MFMA section (SCHED 2, the production schedule): in the load
-//     section its ~60-cycle issue cost made that section the critical path
-//     (fc1 shape: 1.25 vs 1.09-1.16 PF; SCHED 1, a non-ping-pong schedule
-//     with the reads interleaved between the MFMAs, 1.06-1.08 PF).
+//     the other wave's fragment reads.  The DMA of subtile p+3 is split
+//     between the two sections (SCHED 3, the production schedule): dY's half
+//     in the load section after the fragment reads, X's half inside the MFMA
+//     section.  Each glds costs ~60 issue cycles: all four in the load section
+//     made it the critical path (SCHED 0, fc1 1.09-1.16 PF), all four in the
+//     MFMA section stall the MFMA pipe (SCHED 2, 1.25-1.31 PF), one per
+//     alternate MFMA row likewise (SCHED 4, 1.21-1.25 PF); split: 1.37 PF on
+//     fc1, 1.47 on qkv, 1.37 on fc2 (profiles/r2f_wgrad_sched.txt).  SCHED 1,
+//     a non-ping-pong schedule with the reads between the MFMAs: 1.06-1.08 PF.
 //   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
 //     0: the first micro-batch of a step; main_grad is never zero-filled),
 //     transposed through LDS so G moves in 16-B row pieces (+1.5 % on fc1
@@ -71,11 +75,11 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 
 // Stage the [32 m][256] slice of a row-major [M][ld] matrix (cols c0..c0+255,
 // rows m0..m0+31) at LDS byte offset `dst`: 16 pieces of 1 KiB, 2 per wave.
-template <typename T>
+template <typename T, int I0 = 0, int I1 = 2>
 __device__ __forceinline__ void stage_op(const T* __restrict__ src, int64_t ld, int64_t m0,
                                          int64_t c0, char* lds, int dst, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = I0; i < I1; ++i) {
     const int piece = wave * 2 + i;
     const int o = piece * 1024 + lane * 16;  // LDS byte this lane's 16 B land on
     const int rem = o & 4095;
@@ -108,25 +112,19 @@ __device__ __forceinline__ void wait_subtiles(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Grouped tile order: lin -> (tn, tk).  gn > 0: groups of gn n-tiles x all
-// k-tiles, n fastest; gn < 0: groups of -gn k-tiles x all n-tiles, k fastest.
-__device__ __forceinline__ void tile_of(int lin, int ntn, int ntk, int gn, int& tn, int& tk) {
-  if (gn > 0) {
-    const int grp = lin / (gn * ntk);
-    const int first_n = grp * gn;
-    const int gsize = min(gn, ntn - first_n);
-    const int in_grp = lin - grp * gn * ntk;
-    tn = first_n + in_grp % gsize;
-    tk = in_grp / gsize;
-  } else {
-    const int gk = -gn;
-    const int grp = lin / (gk * ntn);
-    const int first_k = grp * gk;
-    const int gsize = min(gk, ntk - first_k);
-    const int in_grp = lin - grp * gk * ntn;
-    tk = first_k + in_grp % gsize;
-    tn = in_grp / gsize;
-  }
+// Grouped tile order: lin -> (tn, tk) as (x, y).  gn > 0: groups of gn n-tiles
+// x all k-tiles, n fastest; gn < 0: groups of -gn k-tiles x all n-tiles, k
+// fastest.  Returned by value (out-references were lowered through scratch).
+__device__ __forceinline__ int2 tile_of(int lin, int ntn, int ntk, int gn) {
+  const bool byn = gn > 0;
+  const int g = byn ? gn : -gn;
+  const int nlong = byn ? ntk : ntn, nshort = byn ? ntn : ntk;
+  const int grp = lin / (g * nlong);
+  const int first = grp * g;
+  const int gsize = min(g, nshort - first);
+  const int in_grp = lin - grp * g * nlong;
+  const int a = first + in_grp % gsize, b = in_grp / gsize;
+  return byn ? int2{a, b} : int2{b, a};
 }
 
 template <typename T>
@@ -154,8 +152,8 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   // splits in order (deterministic)
   const int split = (int)blockIdx.x / nlin;
   const int lin = lin0 + xcd_remap((int)blockIdx.x - split * nlin, nlin);
-  int tn, tk;
-  tile_of(lin, ntn, ntk, gn, tn, tk);
+  const int2 tt = tile_of(lin, ntn, ntk, gn);
+  const int tn = tt.x, tk = tt.y;
   int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
   int ldg = K;  // row stride of the output
   if (ws) {
@@ -229,6 +227,29 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
 #pragma unroll
       for (int j = 0; j < FB_; ++j) acc[I][j] = mfma16<T>(av[I], bv[j], acc[I][j]);
       // SCHED 2: the DMA of subtile t+3 rides in the MFMA section (rows 1, 5)
+      // SCHED 3: only X's half does (row 3); dY's was issued in the load section
+      // SCHED 4: one DMA instruction per MFMA row 0, 2, 4, 6
+      if constexpr (SCHED == 3 && MODE != 2 && I == 3) {
+        const int ts = t + NSLOT - 1;
+        if (ts < nt) {
+          __builtin_amdgcn_sched_barrier(0);
+          stage_op<T>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (SCHED == 4 && MODE != 2 && (I % 2 == 0)) {
+        const int ts = t + NSLOT - 1;
+        if (ts < nt) {
+          __builtin_amdgcn_sched_barrier(0);
+          constexpr int P = (I / 2) & 1;
+          if constexpr (I < 4)
+            stage_op<T, P, P + 1>(dy, N, (int64_t)ts * BM, n0, lds, (ts % NSLOT) * SLOTB, wave, lane);
+          else
+            stage_op<T, P, P + 1>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave,
+                                  lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       if constexpr (SCHED == 2 && MODE != 2 && (I == 1 || I == 5)) {
         const int ts = t + NSLOT - 1;
         if (ts < nt) {
@@ -267,6 +288,16 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     if constexpr (SCHED == 0) {
       if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
       wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
+    } else if constexpr (SCHED == 3) {
+      // dY half of subtile t+3 here (2 DMA instructions behind subtile t+2)
+      if (t + NSLOT - 1 < nt) {
+        if constexpr (MODE != 2)
+          stage_op<T>(dy, N, (int64_t)(t + NSLOT - 1) * BM, n0, lds, ((t + NSLOT - 1) % NSLOT) * SLOTB,
+                      wave, lane);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
+      }
     } else {
       wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
     }
@@ -432,8 +463,8 @@ __global__ __launch_bounds__(256) void wgrad_split_reduce_k(const float* __restr
                                                            int gn, int lin0, int nlin, int nsplit,
                                                            int accumulate) {
   const int t = blockIdx.x / 64, part = blockIdx.x % 64;
-  int tn, tk;
-  tile_of(lin0 + t, N / TN, K / TK, gn, tn, tk);
+  const int2 tt = tile_of(lin0 + t, N / TN, K / TK, gn);
+  const int tn = tt.x, tk = tt.y;
   const int e = (part * 256 + threadIdx.x) * 4;  // element of the 256 x 256 block
   const int row = e / TK, col = e % TK;
   float* gp = g + ((int64_t)tn * TN + row) * K + (int64_t)tk * TK + col;
@@ -452,7 +483,11 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
                          int64_t K, int mode, hipStream_t s) {
   const int m = mode % 10, v = mode / 10;
   const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (v == 2) {
+  if (v == 3) {
+    launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 4) {
+    launch<bf16, true, 0, 4>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 2) {
     if (m == 1) launch<bf16, true, 1, 2>(dy, x, g, iM, iN, iK, s);
     else if (m == 2) launch<bf16, true, 2, 2>(dy, x, g, iM, iN, iK, s);
     else launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
@@ -522,18 +557,18 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
   if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (accumulate) launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     } else if (dt == DT_F16) {
-      if (accumulate) launch<fp16, true, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<fp16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<fp16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     }
   }
   if (split) {
     if (dt == DT_BF16)
-      launch<bf16, false, 0, 2>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     else if (dt == DT_F16)
-      launch<fp16, false, 0, 2>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<fp16, false, 0, 3>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
                        ws, g, iN, iK, tile_group(iN / TN, iK / TK), pl.tail_lin0, pl.tail_tiles,
                        pl.nsplit, accumulate ? 1 : 0);

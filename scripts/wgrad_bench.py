@@ -70,6 +70,9 @@ def ablation(modes=(0, 1, 2)):
     loads; mode // 10 = schedule variant.  Checks each variant's numerics first."""
     C = ext()
     M, N, K = 16384, 22016, 4096
+    if os.environ.get("WG_SHAPE"):  # "N,K" (default: the 7B fc1 wgrad)
+        N, K = (int(v) for v in os.environ["WG_SHAPE"].split(","))
+    print(f"ablation shape M={M} N={N} K={K}", flush=True)
     dY = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) - 0.5
     X = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) - 0.5
     G = torch.zeros(N, K, device="cuda", dtype=torch.float32)
