@@ -594,8 +594,13 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
 void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
                   int64_t b, int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
                   std::vector<int64_t> qs, std::vector<int64_t> ks, std::vector<int64_t> vs,
-                  std::vector<int64_t> os, double scale) {
+                  std::vector<int64_t> os, double scale, const c10::optional<at::Tensor>& kv_len) {
   check_gpu(q, "q");
+  if (kv_len) {
+    TORCH_CHECK(kv_len->is_cuda() && kv_len->scalar_type() == at::kInt && kv_len->numel() >= 1,
+                "kv_len must be a device int32 tensor");
+    TORCH_CHECK(kv_len->device() == q.device(), "kv_len on another device");
+  }
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
               out.scalar_type() == q.scalar_type(), "q/k/v/out dtype mismatch");
   TORCH_CHECK(ema::flash_attn_supported((int)hd, dtype_code(q)), "decode attention supports "
@@ -620,6 +625,7 @@ void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   p.v_sb = vs[0]; p.v_ss = vs[1]; p.v_sg = vs[2];
   p.o_sb = os[0]; p.o_sh = os[2];
   p.scale = (float)scale;
+  p.kv_len = kv_len ? kv_len->data_ptr<int>() : nullptr;
   const int64_t ns = ema::flash_decode_splits((int)sk);
   auto ws = at::empty({b * nq * ns * (hd + 2)}, q.options().dtype(at::kFloat));
   p.ws_o = ws.data_ptr<float>();

@@ -19,6 +19,10 @@
 //   pass 2 (one thread per output element group): rescale-and-sum the chunk
 //     partials in chunk order (deterministic) and write O.
 //
+// With a device-side key count (DecodeParams::kv_len) the launch is
+// independent of the step, so the whole decode step can be captured once in
+// a hipGraph and replayed (inference/hip_graph.py).
+//
 // Used when it beats the FlashAttention forward on one query row (ops/attention.py
 // flash_attn_func): GQA/MQA (r >= 2: each K/V byte is read once, not r times)
 // and small grids (nq * b < 256); MHA with a full grid stays on FlashAttention
@@ -35,9 +39,10 @@ namespace ema {
 namespace {
 
 constexpr int DCH = 256;  // keys per chunk (= threads per workgroup)
-constexpr int RH = 8;     // query heads per workgroup
+// RH: query heads per workgroup = min(8, heads per KV group) rounded up to a
+// power of two (MHA: 1, so no lane computes scores for absent heads)
 
-template <typename T, int HD>
+template <typename T, int HD, int RH>
 __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   constexpr int HP = HD / 64;  // head-dim elements per lane in P.V (1 or 2)
   __shared__ float qs[RH][HD];
@@ -51,8 +56,22 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   const int g = blockIdx.y / nhs, hs = blockIdx.y % nhs, b = blockIdx.z;
   const int h0 = hs * RH, nh = min(RH, r - h0);  // heads g*r + h0 .. + nh - 1
   const int k0 = chunk * DCH;
-  const int nk = min(DCH, p.sk - k0);
+  const int sk = p.kv_len ? min(*p.kv_len, p.sk) : p.sk;
+  const int nk = min(DCH, sk - k0);
   const float sl2 = p.scale * 1.4426950408889634f;
+  if (nk <= 0) {  // chunk past the cached length (hipGraph decode): empty partial
+    const int nsplit = gridDim.x;
+    for (int i = tid; i < nh * HD; i += 256) {
+      const int head = g * r + h0 + i / HD;
+      p.ws_o[(((int64_t)b * p.nq + head) * nsplit + chunk) * HD + i % HD] = 0.f;
+    }
+    if (tid < nh) {
+      const int64_t idx = ((int64_t)b * p.nq + g * r + h0 + tid) * nsplit + chunk;
+      p.ws_ml[2 * idx] = -INFINITY;
+      p.ws_ml[2 * idx + 1] = 0.f;
+    }
+    return;
+  }
 
   // query vectors of this slice -> LDS (fp32)
   for (int i = tid; i < RH * HD; i += 256) {
@@ -191,11 +210,20 @@ __global__ __launch_bounds__(256) void decode_combine_k(const DecodeParams p, in
   *reinterpret_cast<typename fa::MT<T>::x4*>(out) = w4;
 }
 
+template <typename T, int HD, int RH>
+void launch_partial(const DecodeParams& p, int nsplit, hipStream_t s) {
+  const int r = p.nq / p.nkv, nhs = (r + RH - 1) / RH;
+  hipLaunchKernelGGL((decode_partial_k<T, HD, RH>), dim3(nsplit, p.nkv * nhs, p.b), dim3(256), 0, s, p);
+}
+
 template <typename T, int HD>
 void launch(const DecodeParams& p, hipStream_t s) {
-  const int r = p.nq / p.nkv, nhs = (r + RH - 1) / RH;
+  const int r = p.nq / p.nkv;
   const int nsplit = flash_decode_splits(p.sk);
-  hipLaunchKernelGGL((decode_partial_k<T, HD>), dim3(nsplit, p.nkv * nhs, p.b), dim3(256), 0, s, p);
+  if (r >= 8) launch_partial<T, HD, 8>(p, nsplit, s);
+  else if (r >= 4) launch_partial<T, HD, 4>(p, nsplit, s);
+  else if (r >= 2) launch_partial<T, HD, 2>(p, nsplit, s);
+  else launch_partial<T, HD, 1>(p, nsplit, s);
   const int64_t total = (int64_t)p.b * p.nq * (HD / 4);
   hipLaunchKernelGGL((decode_combine_k<T, HD>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      s, p, nsplit);

@@ -161,6 +161,10 @@ struct DecodeParams {
   float scale;
   float* ws_o;   // fp32 [b][nq][splits][hd] chunk partials
   float* ws_ml;  // fp32 [b][nq][splits][2] chunk (max, sum) in log2 units
+  // optional device int32: the number of valid keys (<= sk).  The grid is
+  // sized for sk (the cache capacity) and chunks past the length exit early,
+  // so one launch serves every step of a captured hipGraph decode loop.
+  const int* kv_len;
 };
 int flash_decode_splits(int sk);
 void flash_decode(const DecodeParams& p, int dt, hipStream_t s);

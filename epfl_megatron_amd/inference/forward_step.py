@@ -26,6 +26,10 @@ class InferenceParams:
         self.sequence_len_offset = 0
         self.batch_size_offset = 0
         self.key_value_memory_dict = {}
+        # hipGraph decode (inference/hip_graph.py): the cache slot of the new
+        # token (int64 [1]) and the valid key count (int32 [1]) on the device
+        self.device_offset = None
+        self.device_kv_len = None
 
     def swap_key_value_dict(self, batch_idx):
         """Reorder the cached batch rows (beam search keeps the best beams)."""

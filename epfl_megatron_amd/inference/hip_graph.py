@@ -1,0 +1,116 @@
+"""hipGraph-captured decode step for KV-cached generation on MI355X.
+
+One token-by-token decode step of Llama-2-7B issues ~450 small launches
+(per layer: fused-QKV skinny GEMM, RoPE, two cache writes, split-key decode
+attention + combine, dense, residual-norm, fc1, SwiGLU, fc2, ...).  At batch 1
+the step is bound by the host issuing them, not by the 13.5 GB weight stream
+(``profiles/r2e_serve_bench_llama7b.txt``: 4.79 ms/step eager).  The step
+below is captured ONCE into a HIP graph (``torch.cuda.CUDAGraph`` is a
+hipGraph on ROCm) and replayed: no Python, no per-kernel launch cost.
+
+What makes the step capturable: nothing in it depends on the step on the host.
+  * the token's cache slot and the number of valid keys are device tensors
+    (``InferenceParams.device_offset`` / ``device_kv_len``): the K/V write is
+    an ``index_copy_`` and the decode attention reads the key count on the
+    device (``csrc/flash_decode.hip``, grid sized for the whole cache, chunks
+    past the length exit early);
+  * RoPE takes the absolute position ids (a static device tensor);
+  * greedy selection (argmax), the position / slot / length increments and
+    the write into the generated-token history are part of the graph.
+
+The reference decodes eagerly (``megatron/text_generation/generation.py``
+drives ``forward_step.py`` once per token); this is an MI355X-side addition.
+Single model-parallel rank (TP = PP = 1) only: the graph holds no collectives.
+"""
+import torch
+
+from ..parallel import state
+
+
+class GraphedGreedyDecoder:
+    """Greedy decode of ``batch`` sequences whose prompts were prefilled into
+    ``inference_params`` (eagerly, e.g. one ``model(prompt, ...)`` call).
+
+    Usage::
+
+        dec = GraphedGreedyDecoder(model, ip, batch, max_new_tokens)
+        dec.start(next_tokens, position)   # first new token, its position
+        for _ in range(n):
+            dec.step()                     # one replay = one generated token
+        tokens = dec.history[:, :n]        # [batch, n] (device)
+    """
+
+    def __init__(self, model, inference_params, batch, max_new_tokens):
+        if state.model_parallel_is_initialized() and (
+                state.get_tensor_model_parallel_world_size() > 1
+                or state.get_pipeline_model_parallel_world_size() > 1):
+            raise NotImplementedError("hipGraph decode runs on a single model-parallel rank")
+        if not torch.cuda.is_available():
+            raise RuntimeError("hipGraph decode needs a GPU")
+        self.model = model
+        self.ip = inference_params
+        self.batch = batch
+        self.max_new = max_new_tokens
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.tokens = torch.zeros(batch, 1, dtype=torch.long, device=dev)
+        self.pos = torch.zeros(batch, 1, dtype=torch.long, device=dev)
+        self.step_idx = torch.zeros(1, dtype=torch.long, device=dev)
+        self.history = torch.zeros(batch, max_new_tokens + 1, dtype=torch.long, device=dev)
+        self.ip.device_offset = torch.zeros(1, dtype=torch.long, device=dev)
+        self.ip.device_kv_len = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = None
+        self.logits = None
+        self.steps_done = 0
+
+    def _forward(self):
+        return self.model(self.tokens, self.pos, None, inference_params=self.ip)
+
+    def _body(self):
+        logits = self._forward()
+        nxt = logits[:, -1].argmax(-1, keepdim=True)
+        self.history.index_copy_(1, self.step_idx, nxt)
+        self.tokens.copy_(nxt)
+        self.pos.add_(1)
+        self.step_idx.add_(1)
+        self.ip.device_offset.add_(1)
+        self.ip.device_kv_len.add_(1)
+        return logits
+
+    def start(self, next_tokens, position):
+        """Set the first token to feed (``[batch, 1]``) at absolute ``position``
+        (= the number of tokens already cached) and capture the graph on the
+        first call."""
+        if position + self.max_new > self.ip.max_sequence_len:
+            raise ValueError("KV cache too short for max_new_tokens")
+        with torch.no_grad():
+            self.tokens.copy_(next_tokens.view(self.batch, 1))
+            self.pos.fill_(position)
+            self.step_idx.zero_()
+            self.ip.device_offset.fill_(position)
+            self.ip.device_kv_len.fill_(position + 1)
+            if self.graph is None:
+                self._capture()
+        self.base = position
+        self.steps_done = 0
+
+    def _capture(self):
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            # warm-up at the current state: writes the cache slot the first
+            # replay writes again (idempotent), initialises lazy state
+            self._forward()
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = self._body()
+
+    def step(self):
+        if self.steps_done >= self.max_new:
+            raise RuntimeError("max_new_tokens reached")
+        self.graph.replay()
+        self.steps_done += 1
+        self.ip.sequence_len_offset = self.base + self.steps_done
+        return self.tokens

@@ -33,7 +33,7 @@ from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm
 from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
 from ..ops._ext import use_native
-from ..ops.attention import flash_attn_qkvpacked, flash_attn_func
+from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
 from ..ops.activations import glu, bias_gelu, gelu
 from ..ops.softmax import FusedScaleMaskSoftmax
 from .enums import AttnMaskType, AttnType, LayerType, ModelType, PositionEmbeddingType
@@ -296,6 +296,15 @@ class ParallelAttention(MegatronModule):
             # Rotate with the true positions BEFORE caching (fixes D1).
             q = apply_rope_ref(q, rope[0], rope[1], position_ids, offset=s0)
             k = apply_rope_ref(k, rope[0], rope[1], position_ids, offset=s0)
+        if getattr(ip, "device_offset", None) is not None and sq == 1:
+            # hipGraph decode step (inference/hip_graph.py): cache slot and key
+            # count live in device tensors, so no launch depends on the step
+            kc, vc = kmem[:, b0:b0 + b], vmem[:, b0:b0 + b]
+            kc.index_copy_(0, ip.device_offset, k)
+            vc.index_copy_(0, ip.device_offset, v)
+            o = flash_decode_cached(q.transpose(0, 1), kc.transpose(0, 1), vc.transpose(0, 1),
+                                    ip.device_kv_len)
+            return o.transpose(0, 1).reshape(sq, b, -1)
         kmem[s0:s0 + sq, b0:b0 + b] = k
         vmem[s0:s0 + sq, b0:b0 + b] = v
         keys = kmem[:s0 + sq, b0:b0 + b]

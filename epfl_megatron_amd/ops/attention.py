@@ -132,17 +132,30 @@ class _FlashQKVPackedFn(torch.autograd.Function):
         return dqkv5.view(s, b, -1), None, None, None, None, None, None, None, None
 
 
-def _flash_decode(q, k, v, scale):
+def _flash_decode(q, k, v, scale, kv_len=None):
     """sq == 1 against a KV cache (generation): split-key decode kernel
-    (``csrc/flash_decode.hip``); no autograd."""
+    (``csrc/flash_decode.hip``); no autograd.  ``kv_len``: optional device
+    int32 tensor with the number of valid keys (k / v then span the whole
+    cache; the launch does not depend on the step, for hipGraph capture)."""
     b, _, nq, d = q.shape
     sk, nkv = k.shape[1], k.shape[2]
     r = nq // nkv
     out = torch.empty(b, 1, nq, d, dtype=q.dtype, device=q.device)
     ext().flash_decode(q, k, v, out, b, sk, nq, nkv, d, list(_bsnd_strides(q, r)),
                        list(_bsnd_strides(k, 1)[:3]), list(_bsnd_strides(v, 1)[:3]),
-                       [out.stride(0), out.stride(1), out.stride(2)], float(scale))
+                       [out.stride(0), out.stride(1), out.stride(2)], float(scale), kv_len)
     return out
+
+
+def flash_decode_cached(q, k, v, kv_len, softmax_scale=None):
+    """One query row per sequence against a whole KV cache ``k / v [b, smax,
+    nkv, d]`` of which the first ``kv_len`` (device int32) keys are valid."""
+    if not use_native(q):
+        n = int(kv_len.reshape(-1)[0])
+        return attention_ref(q, k[:, :n], v[:, :n], False,
+                             softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1]))
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    return _flash_decode(q, k, v, scale, kv_len)
 
 
 class _FlashFn(torch.autograd.Function):
@@ -210,10 +223,10 @@ def flash_attn_func(q, k, v, causal=True, softmax_scale=None):
     if use_native(q):
         b, sq, nq = q.shape[:3]
         r = nq // k.shape[2]
-        if sq == 1 and (r >= 2 or nq * b < 256) and not (
+        if sq == 1 and (r >= 2 or nq * b < 256 or k.shape[1] <= 512) and not (
                 torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)):
             # split-key decode: GQA/MQA reads each K/V byte once; small grids
-            # spread over the chunks (profiles/r2c_decode_bench.txt)
+            # spread over the chunks; short caches (profiles/r2f_decode_bench.txt)
             return _flash_decode(q, k, v, scale)  # the last position sees every cached key
         return _FlashFn.apply(q, k, v, causal, scale)
     return attention_ref(q, k, v, causal, scale)

@@ -39,5 +39,6 @@ def bench(b, sk, nq, nkv, hd):
 
 if __name__ == "__main__":
     for sh in ((1, 2048, 32, 32, 128), (8, 2048, 32, 32, 128), (1, 4096, 64, 8, 128),
-               (16, 4096, 64, 8, 128), (4, 2048, 71, 1, 64)):
+               (16, 4096, 64, 8, 128), (4, 2048, 71, 1, 64), (1, 256, 32, 32, 128),
+               (8, 256, 32, 32, 128), (32, 256, 32, 32, 128)):
         bench(*sh)

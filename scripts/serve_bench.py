@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--graph", action="store_true",
+                    help="decode steps replayed from one captured hipGraph (inference/hip_graph.py)")
     a = ap.parse_args()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29561"),
                       RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
@@ -35,6 +37,7 @@ def main():
     from epfl_megatron_amd.models import ModelType
     from epfl_megatron_amd.training import get_model
     from epfl_megatron_amd.inference.forward_step import InferenceParams
+    from epfl_megatron_amd.inference.hip_graph import GraphedGreedyDecoder
 
     argv = ["--num_layers", str(a.layers), "--hidden_size", "4096", "--num_attention_heads", "32",
             "--ffn_hidden_size", "11008", "--seq_length", "4096", "--max_position_embeddings",
@@ -54,23 +57,34 @@ def main():
         prompt = torch.randint(0, 32000, (B, a.prompt), device="cuda")
         pos = torch.arange(total, device="cuda")[None].expand(B, -1)
         with torch.no_grad():
+            ip = InferenceParams(B, total)
             for rep in range(2):  # rep 0 warms up allocator / kernels
-                ip = InferenceParams(B, total)
+                if not a.graph:
+                    ip = InferenceParams(B, total)
+                ip.sequence_len_offset = 0  # graph mode: same caches, prefill again
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 logits = m(prompt, pos[:, :a.prompt], None, inference_params=ip)
                 nxt = logits[:, -1].argmax(-1, keepdim=True)
                 ip.sequence_len_offset += a.prompt
+                if a.graph:  # capture (rep 0) / re-prime, outside the timed region
+                    if rep == 0:
+                        dec = GraphedGreedyDecoder(m, ip, B, a.gen)
+                    dec.start(nxt, a.prompt)
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
-                for t in range(a.prompt, total - 1):
-                    logits = m(nxt, pos[:, t:t + 1], None, inference_params=ip)
-                    nxt = logits[:, -1].argmax(-1, keepdim=True)
-                    ip.sequence_len_offset += 1
+                if a.graph:
+                    for _ in range(a.prompt, total - 1):
+                        dec.step()
+                else:
+                    for t in range(a.prompt, total - 1):
+                        logits = m(nxt, pos[:, t:t + 1], None, inference_params=ip)
+                        nxt = logits[:, -1].argmax(-1, keepdim=True)
+                        ip.sequence_len_offset += 1
                 torch.cuda.synchronize()
                 t2 = time.perf_counter()
         steps = a.gen - 1
-        r = {"batch": B, "prompt": a.prompt, "gen": a.gen, "prefill_ms": round(1e3 * (t1 - t0), 2),
+        r = {"batch": B, "graph": bool(a.graph), "prompt": a.prompt, "gen": a.gen, "prefill_ms": round(1e3 * (t1 - t0), 2),
              "decode_ms_per_step": round(1e3 * (t2 - t1) / steps, 3),
              "decode_tokens_per_s": round(B * steps / (t2 - t1), 1)}
         print(json.dumps(r), flush=True)

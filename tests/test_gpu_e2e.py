@@ -154,3 +154,62 @@ def _kv_decode(rank, world):
 def test_gpu_kv_cached_decode_matches_full_forward():
     err, scale = run_dist(_kv_decode, 1)[0]
     assert err < 3e-2 * max(1.0, scale), (err, scale)
+
+
+def _graph_decode(rank, world):
+    """Greedy generation replayed from one captured hipGraph (device-side cache
+    slot / key count, argmax and increments inside the graph) vs the eager
+    KV-cached greedy loop: same tokens, and logits of the last step close."""
+    import finetune
+    init_framework(LLAMA_GQA + ["--bf16"], finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.training import get_model
+    from epfl_megatron_amd.inference.forward_step import InferenceParams
+    from epfl_megatron_amd.inference.hip_graph import GraphedGreedyDecoder
+    args = get_args()
+    model = get_model(finetune.model_provider, ModelType.encoder_or_decoder, wrap_with_ddp=False)
+    _deterministic_init(model, args)
+    m = model[0].eval()
+    torch.manual_seed(5)
+    b, plen, n, cap = 2, 29, 10, 600  # cache longer than one 256-key chunk
+    prompt = torch.randint(0, 512, (b, plen), device="cuda")
+    pos = torch.arange(cap, device="cuda")[None].expand(b, -1)
+    with torch.no_grad():
+        ip = InferenceParams(b, cap)
+        nxt = m(prompt, pos[:, :plen], None, inference_params=ip)[:, -1].argmax(-1, keepdim=True)
+        ip.sequence_len_offset += plen
+        first = nxt.clone()
+        eager = []
+        for t in range(plen, plen + n):
+            logits_e = m(nxt, pos[:, t:t + 1], None, inference_params=ip)
+            nxt = logits_e[:, -1].argmax(-1, keepdim=True)
+            eager.append(nxt)
+            ip.sequence_len_offset += 1
+        eager = torch.cat(eager, dim=1)
+
+        ip2 = InferenceParams(b, cap)
+        m(prompt, pos[:, :plen], None, inference_params=ip2)
+        ip2.sequence_len_offset += plen
+    dec = GraphedGreedyDecoder(m, ip2, b, n)
+    dec.start(first, plen)
+    for _ in range(n):
+        dec.step()
+    torch.cuda.synchronize()
+    graphed = dec.history[:, :n]
+    # a second generation through the same graph (re-primed, not re-captured)
+    dec.start(first, plen)
+    for _ in range(n):
+        dec.step()
+    again = dec.history[:, :n]
+    lerr = float((dec.logits.float() - logits_e.float()).abs().max())
+    return (graphed.cpu().tolist(), again.cpu().tolist(), eager.cpu().tolist(), lerr,
+            float(logits_e.float().abs().max()))
+
+
+@pytest.mark.gpu
+def test_gpu_hip_graph_greedy_decode_matches_eager():
+    graphed, again, eager, lerr, scale = run_dist(_graph_decode, 1)[0]
+    assert graphed == eager, (graphed, eager)
+    assert again == eager
+    assert lerr < 2e-2 * max(1.0, scale), (lerr, scale)
