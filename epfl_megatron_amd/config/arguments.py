@@ -46,6 +46,9 @@ FLAG_TABLE = {
     "inference": [
         _flag("--inference_batch_times_seqlen_threshold", type=int, default=512),
         _flag("--max_tokens_to_oom", type=int, default=12000),
+        _flag("--inference_hip_graph", action="store_true",
+              help="replay single-token decode forwards from a captured hipGraph "
+                   "(TP = PP = 1; inference/hip_graph.py)"),
     ],
     "network size": [
         _flag("--num_layers", type=int, default=None),

@@ -38,7 +38,10 @@ class InferenceParams:
         for layer, (k, v) in self.key_value_memory_dict.items():
             if len(batch_idx) != k.shape[1]:
                 raise AssertionError("batch size mismatch while reordering the KV cache")
-            self.key_value_memory_dict[layer] = (k[:, batch_idx], v[:, batch_idx])
+            # in place: a captured hipGraph (inference/hip_graph.py) holds
+            # these cache addresses
+            k.copy_(k[:, batch_idx])
+            v.copy_(v[:, batch_idx])
 
 
 class ForwardStep:
@@ -52,8 +55,18 @@ class ForwardStep:
         args = global_vars.get_args()
         self.pipelined = args.pipeline_model_parallel_size > 1
         self.threshold = args.inference_batch_times_seqlen_threshold
+        self.graphed = None
+        if getattr(args, "inference_hip_graph", False):
+            from .hip_graph import GraphedDecodeForward, graph_decode_supported
+            if graph_decode_supported():
+                self.graphed = GraphedDecodeForward(model, self.inference_params, max_batch_size)
 
     def __call__(self, tokens, position_ids, attention_mask):
+        if self.graphed is not None and tokens.size(1) == 1 and \
+                tokens.size(0) == self.inference_params.max_batch_size:
+            out = self.graphed(tokens, position_ids)
+            self.inference_params.sequence_len_offset += 1
+            return out
         if self.pipelined and tokens.size(0) * tokens.size(1) >= self.threshold:
             mbs = max(1, self.threshold // tokens.size(1))
             return _with_pipelining_forward_step(self.model, tokens, position_ids,

@@ -213,3 +213,27 @@ def test_gpu_hip_graph_greedy_decode_matches_eager():
     assert graphed == eager, (graphed, eager)
     assert again == eager
     assert lerr < 2e-2 * max(1.0, scale), (lerr, scale)
+
+
+def _gen_api(rank, world, graph):
+    """Text-generation API (variable prompt lengths, greedy, log-probs) with
+    and without ``--inference_hip_graph``."""
+    from test_inference import _setup, PROMPTS
+    from epfl_megatron_amd.inference import generate_and_post_process
+    # RCCL backend: the inference API keeps its tensors on the CPU under gloo
+    argv = LLAMA_GQA + ["--bf16", "--micro_batch_size", "1", "--global_batch_size", "1",
+                        "--distributed_backend", "nccl"]
+    model = _setup(argv + (["--inference_hip_graph"] if graph else []))
+    texts, segs, logp, tokens = generate_and_post_process(
+        model, prompts=PROMPTS, tokens_to_generate=8, return_output_log_probs=True,
+        top_k_sampling=1, use_eod_token_for_early_termination=False)
+    return tokens, logp
+
+
+@pytest.mark.gpu
+def test_gpu_generation_api_hip_graph_matches_eager():
+    eager_tokens, eager_lp = run_dist(_gen_api, 1, False)[0]
+    graph_tokens, graph_lp = run_dist(_gen_api, 1, True)[0]
+    assert graph_tokens == eager_tokens
+    for a, b in zip(graph_lp, eager_lp):
+        assert a == pytest.approx(b, abs=1e-2)
