@@ -88,8 +88,10 @@ def _check_generation(res, ref, n=6):
         assert got_lp[plen - 1:plen - 1 + n] == pytest.approx(want_lp, abs=2e-4)
 
 
-def test_kv_cached_greedy_matches_full_forward(greedy_ref):
-    res = run_dist(_generate, 1, [], 6)[0]
+@pytest.mark.parametrize("extra", [[], ["--inference_hip_graph"]])
+def test_kv_cached_greedy_matches_full_forward(greedy_ref, extra):
+    # without a GPU --inference_hip_graph must fall back to the eager step
+    res = run_dist(_generate, 1, extra, 6)[0]
     _check_generation(res, greedy_ref)
 
 
