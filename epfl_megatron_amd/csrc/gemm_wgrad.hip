@@ -25,15 +25,17 @@
 //     differ by instruction immediates: 4 base VGPRs per operand.
 //   * Ping-pong: waves 4..7 run one barrier behind waves 0..3 (two barriers
 //     per phase), so on every SIMD one wave's 32 MFMAs (s_setprio 1) overlap
-//     the other wave's fragment reads.  The DMA of subtile p+3 is split
-//     between the two sections (SCHED 3, the production schedule): dY's half
-//     in the load section after the fragment reads, X's half inside the MFMA
-//     section.  Each glds costs ~60 issue cycles: all four in the load section
-//     made it the critical path (SCHED 0, fc1 1.09-1.16 PF), all four in the
-//     MFMA section stall the MFMA pipe (SCHED 2, 1.25-1.31 PF), one per
-//     alternate MFMA row likewise (SCHED 4, 1.21-1.25 PF); split: 1.37 PF on
-//     fc1, 1.47 on qkv, 1.37 on fc2 (profiles/r2f_wgrad_sched.txt).  SCHED 1,
-//     a non-ping-pong schedule with the reads between the MFMAs: 1.06-1.08 PF.
+//     the other wave's fragment reads.  The 4 DMA pieces of subtile p+3 are
+//     split between the two sections (SCHED 5, the production schedule): dY's
+//     two and X's first in the load section after the fragment reads, X's
+//     second inside the MFMA section.  Each glds costs ~60 issue cycles: all
+//     four in the load section made it the critical path (SCHED 0, fc1
+//     1.09-1.16 PF), all four in the MFMA section stall the MFMA pipe (SCHED
+//     2, 1.25-1.32 PF), one per alternate MFMA row likewise (SCHED 4); splits
+//     of 1 / 2 / 3 pieces in the load section (SCHED 6 / 3 / 5): 1.31-1.44 /
+//     1.34-1.47 / 1.37-1.48 PF on fc1 / qkv / fc2 (profiles/r2f_wgrad_sched.txt,
+//     profiles/r2g_wgrad_sched.txt).  SCHED 1, a non-ping-pong schedule with
+//     the reads between the MFMAs: 1.06-1.08 PF.
 //   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
 //     0: the first micro-batch of a step; main_grad is never zero-filled),
 //     transposed through LDS so G moves in 16-B row pieces (+1.5 % on fc1
@@ -192,6 +194,16 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   };
 
   const int nt = M / BM;
+  // SCHED 3 / 5 / 6: 2 / 3 / 1 of a subtile's 4 DMA pieces (dY 0, dY 1, X 0,
+  // X 1) in the load section, the rest inside the MFMA section
+  constexpr int SPLITL = SCHED == 3 ? 2 : SCHED == 5 ? 3 : SCHED == 6 ? 1 : 0;
+  auto stage_piece = [&](int q, int ts) {
+    const int dst = (ts % NSLOT) * SLOTB;
+    if (q == 0) stage_op<T, 0, 1>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
+    else if (q == 1) stage_op<T, 1, 2>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
+    else if (q == 2) stage_op<T, 0, 1>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
+    else stage_op<T, 1, 2>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
+  };
   if constexpr (SCHED != 1) {
   typename fa::MT<T>::x4 fa_[FA_][2], fb_[FB_][2];
   auto reads = [&](int t) {  // all fragments of subtile t (24 transposed reads)
@@ -229,11 +241,11 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       // SCHED 2: the DMA of subtile t+3 rides in the MFMA section (rows 1, 5)
       // SCHED 3: only X's half does (row 3); dY's was issued in the load section
       // SCHED 4: one DMA instruction per MFMA row 0, 2, 4, 6
-      if constexpr (SCHED == 3 && MODE != 2 && I == 3) {
+      if constexpr (SPLITL > 0 && MODE != 2 && I == 3) {
         const int ts = t + NSLOT - 1;
         if (ts < nt) {
           __builtin_amdgcn_sched_barrier(0);
-          stage_op<T>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave, lane);
+          static_for<4 - SPLITL>([&](auto q) { stage_piece(SPLITL + decltype(q)::value, ts); });
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -288,13 +300,12 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     if constexpr (SCHED == 0) {
       if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
       wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
-    } else if constexpr (SCHED == 3) {
-      // dY half of subtile t+3 here (2 DMA instructions behind subtile t+2)
+    } else if constexpr (SPLITL > 0) {
+      // the first SPLITL DMA pieces of subtile t+3 here (behind subtile t+2's 4)
       if (t + NSLOT - 1 < nt) {
         if constexpr (MODE != 2)
-          stage_op<T>(dy, N, (int64_t)(t + NSLOT - 1) * BM, n0, lds, ((t + NSLOT - 1) % NSLOT) * SLOTB,
-                      wave, lane);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          static_for<SPLITL>([&](auto q) { stage_piece(decltype(q)::value, t + NSLOT - 1); });
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 + SPLITL) : "memory");
       } else {
         wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
       }
@@ -483,7 +494,11 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
                          int64_t K, int mode, hipStream_t s) {
   const int m = mode % 10, v = mode / 10;
   const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (v == 3) {
+  if (v == 5) {
+    launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 6) {
+    launch<bf16, true, 0, 6>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 3) {
     launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s);
   } else if (v == 4) {
     launch<bf16, true, 0, 4>(dy, x, g, iM, iN, iK, s);
@@ -555,20 +570,29 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   const WgradPlan pl = wgrad_plan(M, N, K);
   const bool split = pl.nsplit > 1 && ws != nullptr;
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
+  static const bool sched3 = [] {  // EMA_WGRAD_SCHED=3: the 2 + 2 DMA split (A/B)
+    const char* e = getenv("EMA_WGRAD_SCHED");
+    return e && e[0] == '3';
+  }();
   if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (accumulate) launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (sched3) {
+        if (accumulate) launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+        else launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      } else {
+        if (accumulate) launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+        else launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      }
     } else if (dt == DT_F16) {
-      if (accumulate) launch<fp16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<fp16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<fp16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     }
   }
   if (split) {
     if (dt == DT_BF16)
-      launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     else if (dt == DT_F16)
-      launch<fp16, false, 0, 3>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
                        ws, g, iN, iK, tile_group(iN / TN, iK / TK), pl.tail_lin0, pl.tail_tiles,
                        pl.nsplit, accumulate ? 1 : 0);
