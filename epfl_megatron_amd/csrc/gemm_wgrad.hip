@@ -196,7 +196,9 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   const int nt = M / BM;
   // SCHED 3 / 5 / 6: 2 / 3 / 1 of a subtile's 4 DMA pieces (dY 0, dY 1, X 0,
   // X 1) in the load section, the rest inside the MFMA section
-  constexpr int SPLITL = SCHED == 3 ? 2 : SCHED == 5 ? 3 : SCHED == 6 ? 1 : 0;
+  constexpr int SPLITL = SCHED == 3 ? 2 : (SCHED == 5 || SCHED >= 7) ? 3 : SCHED == 6 ? 1 : 0;
+  // MFMA row after which the MFMA-section pieces issue (SCHED 7 / 8: rows 0 / 6)
+  constexpr int MROW = SCHED == 7 ? 0 : SCHED == 8 ? 6 : 3;
   auto stage_piece = [&](int q, int ts) {
     const int dst = (ts % NSLOT) * SLOTB;
     if (q == 0) stage_op<T, 0, 1>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
@@ -241,7 +243,7 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       // SCHED 2: the DMA of subtile t+3 rides in the MFMA section (rows 1, 5)
       // SCHED 3: only X's half does (row 3); dY's was issued in the load section
       // SCHED 4: one DMA instruction per MFMA row 0, 2, 4, 6
-      if constexpr (SPLITL > 0 && MODE != 2 && I == 3) {
+      if constexpr (SPLITL > 0 && MODE != 2 && I == MROW) {
         const int ts = t + NSLOT - 1;
         if (ts < nt) {
           __builtin_amdgcn_sched_barrier(0);
@@ -494,7 +496,11 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
                          int64_t K, int mode, hipStream_t s) {
   const int m = mode % 10, v = mode / 10;
   const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (v == 5) {
+  if (v == 7) {
+    launch<bf16, true, 0, 7>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 8) {
+    launch<bf16, true, 0, 8>(dy, x, g, iM, iN, iK, s);
+  } else if (v == 5) {
     launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s);
   } else if (v == 6) {
     launch<bf16, true, 0, 6>(dy, x, g, iM, iN, iK, s);
