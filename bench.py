@@ -345,13 +345,18 @@ def main(argv=None):
         if par["recompute"]:
             parallel += f"+recompute_{par['recompute']}"
         label = _label(cfg, shape, a)
+        dtype = "bf16" if on_gpu else "fp32"
         if a.proxy:
             metric = (f"PROXY (1 GPU = one TP rank of {a.proxy}; not the BASELINE metric): "
-                      f"per-rank tokens/s")
+                      f"per-rank tokens/s, {dtype}")
             label = f"{label} [{a.proxy} per-rank proxy]"
-        else:
-            metric = (f"{BASELINE_METRIC} [{label} bf16 training; value = tokens/s aggregate "
+        elif cfg["model"] == "llama2-7b":
+            metric = (f"{BASELINE_METRIC} [{label} {dtype} training; value = tokens/s aggregate "
                       "over all GPUs, per-GPU = value / n_gpus, MFU in 'mfu']")
+        else:  # another BASELINE config: do not claim the Llama-2-7B headline
+            metric = (f"tokens/sec/GPU + MFU, {label} {dtype} training, preset {a.preset} "
+                      "[value = tokens/s aggregate over all GPUs, MFU in 'mfu'; "
+                      "not the headline metric of BASELINE.json]")
         rec = {
             "metric": metric,
             "value": round(tok_s, 1),
@@ -365,7 +370,7 @@ def main(argv=None):
             "vs_baseline": (round(per_gpu / REF_TOKENS_PER_SEC_PER_GPU, 3)
                             if cfg["model"] == "llama2-7b" and par["seq"] == 1024
                             and not a.proxy else None),
-            "dtype": "bf16" if on_gpu else "fp32",
+            "dtype": dtype,
             "data": f"synthetic ({a.data} tokens), random-init weights",
             "config": {"model": label, "global_batch": par["gbs"], "seq_len": par["seq"],
                        "micro_batch": par["mbs"], "num_micro_batches": par["nmicro"],
@@ -378,6 +383,9 @@ def main(argv=None):
             "first_loss": round(float(loss_t[0]), 4),
             "final_loss": round(float(loss_t[1]), 4),
             "max_mem_gb": round(float(mem[0]), 1) if on_gpu else None,
+            "backend": dist.get_backend(),
+            "world_size": world,
+            "dp": par["dp"], "tp": par["tp"], "pp": par["pp"],
         }
         print(json.dumps(rec), flush=True)
     else:

@@ -437,7 +437,14 @@ def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", stri
         optimizer.reload_model_params()
     if not release and not args.finetune and not args.no_load_optim:
         try:
-            if optimizer is not None and optim_sd is not None and "optimizer" in optim_sd:
+            if optimizer is not None and (optim_sd is None or "optimizer" not in optim_sd):
+                # e.g. a checkpoint written without the distributed optimizer
+                # (no optim.pt) or with --no_save_optim: never resume silently
+                # with fresh Adam moments
+                raise KeyError("optimizer state not found" + (
+                    " (no distrib_optim.pt / optim.pt shard for this rank or DP rank 0)"
+                    if args.use_distributed_optimizer else ""))
+            if optimizer is not None:
                 if args.use_distributed_optimizer:
                     it, rel = _read_meta_local(get_checkpoint_tracker_filename(load_dir))
                     optimizer.load_state_dict(optim_sd["optimizer"],
@@ -450,7 +457,7 @@ def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", stri
             print_rank_0(f"Unable to load optimizer from checkpoint {load_dir}: {e}. Specify "
                          "--no_load_optim or --finetune to prevent attempting to load the "
                          "optimizer state, exiting ...")
-            sys.exit()
+            sys.exit(1)
     if not release and not args.finetune and not args.no_load_rng and "rng_state" in model_sd:
         try:
             rs = model_sd["rng_state"]

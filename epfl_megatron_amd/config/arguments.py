@@ -230,6 +230,9 @@ FLAG_TABLE = {
         _flag("--allow_interleaved_pp2", action="store_true",
               help="lift the reference's PP>2 restriction for the interleaved schedule"),
         _flag("--distributed_timeout_minutes", type=int, default=10),
+        _flag("--no_comm_selfcheck", action="store_false", dest="comm_selfcheck",
+              help="skip the startup check of the collectives on the real backend "
+                   "(parallel/selfcheck.py)"),
     ],
     "validation": [
         _flag("--eval_iters", type=int, default=100),

@@ -7,35 +7,10 @@
 // each operand, fp32 math, a single rounding per output.
 #include "common.h"
 #include "kernels.h"
+#include "act_math.h"
 
 namespace ema {
 namespace {
-
-constexpr float kInvSqrt2 = 0.70710678118654752f;
-constexpr float kInvSqrt2Pi = 0.39894228040143268f;
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
-
-template <int KIND>
-__device__ __forceinline__ float act(float x) {
-  if constexpr (KIND == 0) return x * sigmoidf_(x);                     // swiglu
-  else if constexpr (KIND == 1) return 0.5f * x * (1.f + erff(x * kInvSqrt2));  // geglu
-  else if constexpr (KIND == 2) return x > 0.f ? x : 0.f;               // reglu
-  else return x;                                                        // liglu
-}
-template <int KIND>
-__device__ __forceinline__ float dact(float x) {
-  if constexpr (KIND == 0) {
-    const float sg = sigmoidf_(x);
-    return sg * (1.f + x * (1.f - sg));
-  } else if constexpr (KIND == 1) {
-    return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
-  } else if constexpr (KIND == 2) {
-    return x > 0.f ? 1.f : 0.f;
-  } else {
-    return 1.f;
-  }
-}
 
 template <typename T, int KIND>
 __global__ __launch_bounds__(256) void glu_fwd_k(const T* __restrict__ x, T* __restrict__ y,

@@ -720,6 +720,89 @@ void wgrad_gemm_ablation(const at::Tensor& dy, const at::Tensor& x, at::Tensor g
                            cur_stream());
 }
 
+// ---------------------------------------------------------------- NT GEMM
+// 2-D, row stride multiple of 8 elements, unit column stride, 16-B aligned
+static void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 8 == 0,
+              name, ": 2-D with unit column stride and row stride % 8 == 0 required");
+  check_vec_aligned(t, name);
+}
+
+bool gemm_nt_supported(const at::Tensor& a, const at::Tensor& b) {
+  if (!a.is_cuda() || a.dim() != 2 || b.dim() != 2 || a.stride(1) != 1 || b.stride(1) != 1)
+    return false;
+  if (a.scalar_type() != b.scalar_type() ||
+      (a.scalar_type() != at::kBFloat16 && a.scalar_type() != at::kHalf))
+    return false;
+  if (reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(b.data_ptr()) % 16)
+    return false;
+  return a.size(1) == b.size(1) &&
+         ema::gemm_nt_supported(a.size(0), b.size(0), a.size(1), a.stride(0), b.stride(0), b.size(0));
+}
+
+// c[M,N] = a[M,K] b[N,K]^T (c allocated unless given)
+at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::Tensor> out) {
+  check_gpu(a, "a");
+  check_rows(a, "a");
+  check_rows(b, "b");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_nt: a/b dtype mismatch");
+  const int dt = dtype_code(a);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "gemm_nt: bf16/fp16 only");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: reduction dims differ");
+  at::Tensor c = out.has_value() ? *out : at::empty({M, N}, a.options());
+  check_rows(c, "c");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.scalar_type() == a.scalar_type(),
+              "gemm_nt: bad output");
+  TORCH_CHECK(ema::gemm_nt_supported(M, N, K, a.stride(0), b.stride(0), c.stride(0)),
+              "gemm_nt: unsupported shape (K % 32, N % 8)");
+  ema::gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+               c.stride(0), dt, cur_stream());
+  return c;
+}
+
+// fc1 forward with the GLU fused: returns (pre [M, 2F], y [M, F])
+std::vector<at::Tensor> gemm_nt_glu(const at::Tensor& a, const at::Tensor& w1, int64_t kind) {
+  check_gpu(a, "a");
+  check_rows(a, "a");
+  check_rows(w1, "w1");
+  const int dt = dtype_code(a);
+  TORCH_CHECK(a.scalar_type() == w1.scalar_type() && (dt == ema::DT_BF16 || dt == ema::DT_F16),
+              "gemm_nt_glu: bf16/fp16 operands of one dtype");
+  const int64_t M = a.size(0), K = a.size(1), F = w1.size(0) / 2;
+  TORCH_CHECK(w1.size(1) == K && w1.size(0) == 2 * F, "gemm_nt_glu: w1 must be [2F, K]");
+  TORCH_CHECK(ema::gemm_nt_supported(M, F, K, a.stride(0), w1.stride(0), 2 * F),
+              "gemm_nt_glu: unsupported shape (K % 32, F % 8)");
+  auto pre = at::empty({M, 2 * F}, a.options());
+  auto y = at::empty({M, F}, a.options());
+  ema::gemm_nt_glu(a.data_ptr(), w1.data_ptr(), pre.data_ptr(), y.data_ptr(), M, F, K,
+                   a.stride(0), w1.stride(0), (int)kind, dt, cur_stream());
+  return {pre, y};
+}
+
+// fc2 dgrad with the GLU backward fused: d(pre) [M, 2F] from dy [M, K] and
+// w2t = W2^T [F, K] and the saved pre-activation [M, 2F]
+at::Tensor gemm_nt_dglu(const at::Tensor& dy, const at::Tensor& w2t, const at::Tensor& pre,
+                        int64_t kind) {
+  check_gpu(dy, "dy");
+  check_rows(dy, "dy");
+  check_rows(w2t, "w2t");
+  const int dt = dtype_code(dy);
+  TORCH_CHECK(dy.scalar_type() == w2t.scalar_type() && pre.scalar_type() == dy.scalar_type() &&
+              (dt == ema::DT_BF16 || dt == ema::DT_F16), "gemm_nt_dglu: one bf16/fp16 dtype");
+  const int64_t M = dy.size(0), K = dy.size(1), F = w2t.size(0);
+  TORCH_CHECK(w2t.size(1) == K, "gemm_nt_dglu: w2t must be [F, K]");
+  TORCH_CHECK(pre.is_contiguous() && pre.dim() == 2 && pre.size(0) == M && pre.size(1) == 2 * F,
+              "gemm_nt_dglu: pre must be contiguous [M, 2F]");
+  check_vec_aligned(pre, "pre");
+  TORCH_CHECK(ema::gemm_nt_supported(M, F, K, dy.stride(0), w2t.stride(0), 2 * F),
+              "gemm_nt_dglu: unsupported shape (K % 32, F % 8)");
+  auto dpre = at::empty({M, 2 * F}, dy.options());
+  ema::gemm_nt_dglu(dy.data_ptr(), w2t.data_ptr(), pre.data_ptr(), dpre.data_ptr(), M, F, K,
+                    dy.stride(0), w2t.stride(0), (int)kind, dt, cur_stream());
+  return dpre;
+}
+
 // ---------------------------------------------------------------- transpose
 bool transpose16_supported(int64_t rows, int64_t cols) {
   return ema::transpose16_supported(rows, cols);
@@ -752,6 +835,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.def("wgrad_plan", &wgrad_plan);
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_set_variant", &ema::gemm_nt_set_variant);
+  m.def("gemm_nt_glu", &gemm_nt_glu);
+  m.def("gemm_nt_dglu", &gemm_nt_dglu);
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),
         py::arg("res") = py::none());

@@ -1,0 +1,623 @@
+// Forward / data-gradient GEMM for gfx950 (MI355X) with fused GLU epilogues:
+//
+//     C[M, N] = A[M, K] · B[N, K]^T        A, B bf16/fp16 row-major (K contiguous)
+//
+// Every product of a linear layer whose reduction dim is contiguous in both
+// operands is this "NT" form:
+//   * forward  Y  = X · W^T               (A = X,  B = W        [out, in])
+//   * dgrad    dX = dY · W = dY · (W^T)^T  (A = dY, B = W^T      [in, out], the
+//                                          per-step transposed copy of W)
+// and the hand-written kernel replaces hipBLASLt for both, so the MLP's GLU
+// passes disappear into the epilogues (reference MLP megatron/model/
+// transformer.py:92-123, GLU [up; gate] order megatron/model/
+// glu_activations.py:18-21):
+//   EPI_STORE   C = A·B^T (bf16)
+//   EPI_GLU     fc1 forward.  B = W1 [2F, K]; the tile's 256 B rows are 128
+//               "up" rows f0.. and the matching 128 "gate" rows F+f0.., placed
+//               so every lane holds x1 and x2 of the same (m, f) in registers.
+//               Writes the pre-activation [M, 2F] (saved for backward) and
+//               y = x1 * act(x2) [M, F] (the fc2 input).
+//   EPI_DGLU    fc2 dgrad.  C = dAct [M, F] is never written: the epilogue reads
+//               the saved pre-activation and writes d(pre-act) [M, 2F] =
+//               [dAct * act(x2), dAct * x1 * act'(x2)].
+// Numerics equal the unfused path's: the fp32 accumulator is rounded to the
+// operand dtype once, and the GLU math runs in fp32 on those rounded values.
+//
+// Structure (the 256x256 ping-pong of gemm_wgrad.hip, K-contiguous operands):
+//   * 256 (m) x 256 (n) output tile per workgroup, 8 waves as 2 (m) x 4 (n),
+//     each wave 128 x 64 = 8 x 4 tiles of v_mfma_f32_16x16x32, the operands
+//     passed as (B-frag, A-frag) so each lane's accumulator holds 4
+//     CONSECUTIVE output columns of one row (8-byte epilogue pieces).
+//   * K is consumed in subtiles of 32 (one MFMA k-step).  Both [256][32]
+//     operand slices go HBM -> LDS by global_load_lds_dwordx4 into a ring of
+//     4 subtiles (4 x 32 KiB); subtile p+3's loads issue in phase p and are
+//     retired by a counted vmcnt (no vmcnt(0) in the loop).
+//   * LDS image: 64-B rows, 16-B chunk c of row r at 16 (c ^ ((-(r >> 2)) & 3)).
+//     Every ds_read_b128 of an MFMA fragment (16 rows x 4 chunks) then hits
+//     16 distinct 16-B bank slots in each of its 4 lane groups: conflict-free.
+//     The swizzle goes through the per-lane DMA SOURCE address (the DMA writes
+//     LDS lane-linearly), and fragments differ only by instruction immediates.
+//   * Ping-pong: waves 4..7 run one barrier behind waves 0..3, so on every SIMD
+//     one wave's 32 MFMAs (s_setprio 1) overlap the other's fragment reads; 3
+//     of a subtile's 4 DMA pieces issue in the load section, 1 inside the MFMA
+//     section (gemm_wgrad.hip's SCHED 5).
+//   * Epilogue through LDS: each wave rounds its 128 x 64 tile to 16 bits into
+//     a private 16 KiB region (16-B units XOR-swizzled by row), then moves rows
+//     as 16-B pieces (128 B contiguous per 8 lanes).
+//   * XCD-aware grouped tile order: each XCD's 32 concurrent workgroups cover
+//     an 8 (m) x 4 (n) block, sharing A and B panels in its L2.
+// Shapes: K % 32 == 0, N % 8 == 0 (F % 8 for the GLU forms), 16-B aligned rows;
+// ragged M and N tails are clamped on load and masked on store.
+#include <cstdlib>
+
+#include "act_math.h"
+#include "fa_common.h"
+
+namespace ema {
+namespace {
+
+using fa::static_for;
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int TM = 256;               // output rows (m) per tile
+constexpr int TN = 256;               // output cols (n) per tile
+constexpr int BK = 32;                // reduction depth per subtile = one MFMA k-step
+constexpr int OPB = 256 * BK * 2;     // 16 KiB per operand subtile
+constexpr int SLOTB = 2 * OPB;        // A + B
+constexpr int NSLOT = 4;              // ring depth (3 subtiles ahead)
+constexpr int LDSB = NSLOT * SLOTB;   // 128 KiB
+constexpr int FA_ = 8, FB_ = 4;       // m and n fragments per wave
+
+enum { EPI_STORE = 0, EPI_GLU = 1, EPI_DGLU = 2 };
+
+// chunk swizzle of row r (see header)
+__device__ __forceinline__ int rsw(int r) { return (-(r >> 2)) & 3; }
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::MT<T>::x8 b,
+                                        f32x4 c) {
+  if constexpr (__is_same(T, bf16)) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b128 with a folded immediate, as asm so hipcc inserts no vmcnt(0)
+// for the LDS-DMA in flight into other ring slots (consumer waits by hand).
+template <int OFF, typename T>
+__device__ __forceinline__ typename fa::MT<T>::x8 row_read_imm(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  typename fa::MT<T>::x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF));
+  return r;
+}
+
+// Grouped tile order: lin -> (tm, tn).  g > 0: groups of g m-tiles x all
+// n-tiles, m fastest; g < 0: groups of -g n-tiles x all m-tiles, n fastest.
+__device__ __forceinline__ int2 tile_of(int lin, int ntm, int ntn, int g) {
+  const bool bym = g > 0;
+  const int gg = bym ? g : -g;
+  const int nlong = bym ? ntn : ntm, nshort = bym ? ntm : ntn;
+  const int grp = lin / (gg * nlong);
+  const int first = grp * gg;
+  const int gsize = min(gg, nshort - first);
+  const int in_grp = lin - grp * gg * nlong;
+  const int a = first + in_grp % gsize, b = in_grp / gsize;
+  return bym ? int2{a, b} : int2{b, a};
+}
+
+struct NtArgs {
+  const void* a;      // [M, K]
+  const void* b;      // [N, K] (EPI_GLU: [2F, K])
+  void* c;            // EPI_STORE: [M, N]; EPI_GLU: pre-activation [M, 2F]; EPI_DGLU: d(pre) [M, 2F]
+  void* y;            // EPI_GLU: act output [M, F]
+  const void* pre;    // EPI_DGLU: saved pre-activation [M, 2F]
+  int64_t lda, ldb, ldc, ldy;
+  int M, N, K;        // EPI_GLU / EPI_DGLU: N = F
+  int ntm, ntn, gm;
+  bool wave4_ok;      // 32-bit per-lane DMA offsets fit (the 4-wave kernel)
+};
+
+
+// ---- epilogue (both kernels) ------------------------------------------------
+// A wave's 128 x WNC output tile, rounded to 16 bits, sits in LDS as
+// [128 rows][WNC cols] with 16-B unit u of row r stored at unit u ^ (r & (U-1))
+// (U = WNC / 8 units per row).  The accumulator of fragment (i, j) holds row
+// 16 i + (l & 15), cols 16 j + 4 (l >> 4) .. +3 on lane l.
+template <typename T, int FB>
+__device__ __forceinline__ void acc_to_lds(const f32x4 (&acc)[8][FB], char* reg, int lane) {
+  constexpr int U = 2 * FB, RB = 32 * FB;
+  const int r0 = lane & 15, u0 = lane >> 5, h = (lane >> 4) & 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      const int row = 16 * i + r0;
+      const int u = 2 * j + u0;
+      typename fa::MT<T>::x4 v;
+      v[0] = (T)acc[i][j][0]; v[1] = (T)acc[i][j][1];
+      v[2] = (T)acc[i][j][2]; v[3] = (T)acc[i][j][3];
+      *reinterpret_cast<typename fa::MT<T>::x4*>(reg + row * RB + ((u ^ (row & (U - 1))) << 4) + 8 * h) = v;
+    }
+}
+
+// Rows of the LDS tile -> global as 16-B pieces.  gm0: first output row of
+// the wave; gn0: first output column (STORE / DGLU) or first f (GLU: units
+// 0..U/2-1 are up columns f.., units U/2.. the gate columns of the same f).
+template <typename T, int EPI, int ACT, int WNC>
+__device__ __forceinline__ void epilogue_rows(const NtArgs& p, const char* reg, int lane,
+                                              int64_t gm0, int64_t gn0) {
+  constexpr int U = WNC / 8, RB = 2 * WNC;
+  typedef V16<T> V;
+  const int M = p.M, N = p.N;
+  auto unit = [&](int row, int u) {
+    return *reinterpret_cast<const V*>(reg + row * RB + ((u ^ (row & (U - 1))) << 4));
+  };
+  if constexpr (EPI == EPI_GLU) {
+    constexpr int LPR = U / 2, RPI = 64 / LPR, ITERS = 128 / RPI;
+    const int u = lane % LPR;
+    const int64_t f = gn0 + 8 * u;
+    const bool fok = f < N;
+    T* pre = reinterpret_cast<T*>(p.c);
+    T* y = reinterpret_cast<T*>(p.y);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int row = RPI * it + lane / LPR;
+      const V x1 = unit(row, u), x2 = unit(row, u + LPR);
+      V o;
+#pragma unroll
+      for (int e = 0; e < V::N; ++e) o.v[e] = from_f<T>(to_f(x1.v[e]) * act<ACT>(to_f(x2.v[e])));
+      const int64_t gm = gm0 + row;
+      if (fok && gm < M) {
+        st16(pre + gm * p.ldc + f, x1);
+        st16(pre + gm * p.ldc + N + f, x2);
+        st16(y + gm * p.ldy + f, o);
+      }
+    }
+  } else {
+    constexpr int LPR = U, RPI = 64 / LPR, ITERS = 128 / RPI;
+    const int u = lane % LPR;
+    const int64_t gn = gn0 + 8 * u;
+    const bool nok = gn < N;
+    if constexpr (EPI == EPI_STORE) {
+      T* c = reinterpret_cast<T*>(p.c);
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int row = RPI * it + lane / LPR;
+        const V v = unit(row, u);
+        const int64_t gm = gm0 + row;
+        if (nok && gm < M) st16(c + gm * p.ldc + gn, v);
+      }
+    } else {
+      // d(pre) = [g * act(x2), g * x1 * act'(x2)], g = dAct rounded to T
+      const T* pre = reinterpret_cast<const T*>(p.pre);
+      T* d = reinterpret_cast<T*>(p.c);
+      const int64_t gc = nok ? gn : 0;
+#pragma unroll
+      for (int b8 = 0; b8 < ITERS / 8; ++b8) {  // 8 rows of loads in flight
+        V x1[8], x2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int64_t gm = gm0 + RPI * (8 * b8 + k) + lane / LPR;
+          gm = gm < M ? gm : M - 1;
+          x1[k] = ld16(pre + gm * p.ldc + gc);
+          x2[k] = ld16(pre + gm * p.ldc + N + gc);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = RPI * (8 * b8 + k) + lane / LPR;
+          const V g = unit(row, u);
+          const int64_t gm = gm0 + row;
+          V da, dg;
+#pragma unroll
+          for (int e = 0; e < V::N; ++e) {
+            const float gv = to_f(g.v[e]), xg = to_f(x2[k].v[e]);
+            da.v[e] = from_f<T>(gv * act<ACT>(xg));
+            dg.v[e] = from_f<T>(gv * to_f(x1[k].v[e]) * dact<ACT>(xg));
+          }
+          if (nok && gm < M) {
+            st16(d + gm * p.ldc + gn, da);
+            st16(d + gm * p.ldc + N + gn, dg);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int EPI, int ACT>
+__global__ void __launch_bounds__(512, 1) gemm_nt_k(NtArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // wm is also the ping-pong group
+
+  const int ntiles = p.ntm * p.ntn;
+  const int lin = xcd_remap((int)blockIdx.x, ntiles);
+  const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
+  const int64_t m0 = (int64_t)tt.x * TM;
+  // n origin of the tile: output columns (STORE / DGLU) or f (GLU: 128 per tile)
+  const int64_t n0 = (int64_t)tt.y * (EPI == EPI_GLU ? TN / 2 : TN);
+  const int M = p.M, N = p.N;
+
+  // Per-lane DMA source pointers: wave w stages pieces 2w and 2w+1 (16 rows
+  // each) of both operands; lane l lands on row 16 piece + (l >> 2), physical
+  // chunk l & 3 = logical chunk (l & 3) ^ rsw(row) (rsw depends on l >> 4 only).
+  const T* asrc[2];
+  const T* bsrc[2];
+  {
+    const int c = (lane & 3) ^ ((-(lane >> 4)) & 3);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int tr = 16 * (2 * wave + i) + (lane >> 2);  // tile row 0..255
+      int64_t am = m0 + tr;
+      am = am < M ? am : M - 1;
+      asrc[i] = reinterpret_cast<const T*>(p.a) + am * p.lda + 8 * c;
+      int64_t bn;
+      if constexpr (EPI == EPI_GLU) {
+        // tile row -> W1 row: per 64-row wave band, 32 up rows then 32 gate rows
+        const int band = tr >> 6, q = tr & 63;
+        const int64_t f = n0 + 32 * band + (q & 31);
+        bn = f < N ? (q < 32 ? f : N + f) : 0;
+      } else {
+        bn = n0 + tr;
+        bn = bn < N ? bn : N - 1;
+      }
+      bsrc[i] = reinterpret_cast<const T*>(p.b) + bn * p.ldb + 8 * c;
+    }
+  }
+  char* const ldsp = lds;
+  auto stage_piece = [&](int q, int ts) {  // q: 0,1 = A pieces, 2,3 = B pieces
+    const int dst = (ts % NSLOT) * SLOTB + (q >= 2 ? OPB : 0) + (2 * wave + (q & 1)) * 1024;
+    const T* g = (q >= 2 ? bsrc[q & 1] : asrc[q & 1]) + (int64_t)ts * BK;
+    __builtin_amdgcn_global_load_lds((const void*)g,
+                                     (__attribute__((address_space(3))) void*)(ldsp + dst), 16, 0, 0);
+  };
+  auto stage = [&](int ts) {
+    static_for<4>([&](auto q) { stage_piece(decltype(q)::value, ts); });
+  };
+
+  f32x4 acc[FA_][FB_];
+#pragma unroll
+  for (int i = 0; i < FA_; ++i)
+#pragma unroll
+    for (int j = 0; j < FB_; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read bases: row (l & 15) of the wave's band, logical chunk l >> 4
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  const uint32_t fr_off = 64u * (lane & 15) + 16u * ((lane >> 4) ^ rsw(lane & 15));
+  const uint32_t abase = fr_off + 64u * 128u * wm;
+  const uint32_t bbase = OPB + fr_off + 64u * 64u * wn;
+
+  typename fa::MT<T>::x8 fa_[FA_], fb_[FB_];
+  auto reads = [&](int t) {
+    const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
+    const uint32_t a = so + abase, b = so + bbase;
+    static_for<FA_>([&](auto f) {
+      constexpr int F = decltype(f)::value;
+      fa_[F] = row_read_imm<1024 * F, T>(a);
+    });
+    static_for<FB_>([&](auto f) {
+      constexpr int F = decltype(f)::value;
+      fb_[F] = row_read_imm<1024 * F, T>(b);
+    });
+  };
+  const int nt = p.K / BK;
+  auto mfmas = [&](int t) {
+    __builtin_amdgcn_s_setprio(1);
+    static_for<FA_>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+#pragma unroll
+      for (int j = 0; j < FB_; ++j) acc[I][j] = mfma16<T>(fb_[j], fa_[I], acc[I][j]);
+      if constexpr (I == 3) {  // the 4th DMA piece of subtile t+3 rides here
+        const int ts = t + NSLOT - 1;
+        if (ts < nt) {
+          __builtin_amdgcn_sched_barrier(0);
+          stage_piece(3, ts);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+#pragma unroll
+  for (int t = 0; t < NSLOT - 1; ++t)
+    if (t < nt) stage(t);
+  // subtile 0 landed (own DMA): at most min(nt, 3) - 1 subtiles outstanding
+  if (nt >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nt == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();               // ... and everyone's
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+
+  // Phase t: [reads t][3 DMA pieces of t+3][vmcnt: t+1 landed][lgkmcnt(0)]
+  //          BAR_A [32 MFMA + DMA piece 4 of t+3] BAR_B
+  // RAW: subtile t+1 is retired by every wave before its BAR_A(t); both
+  //      groups read it only after a later barrier.
+  // WAR: stage(t+3) overwrites subtile t-1, whose reads every wave retired
+  //      (lgkmcnt(0)) before its BAR_A(t-1), a barrier both groups passed.
+  for (int t = 0; t < nt; ++t) {
+    reads(t);
+    if (t + NSLOT - 1 < nt) {
+      static_for<3>([&](auto q) { stage_piece(decltype(q)::value, t + NSLOT - 1); });
+      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // t+2 (4) and t+3 (3) may fly
+    } else {
+      const int ahead = min(t + NSLOT - 2, nt - 1) - (t + 1);  // subtiles allowed in flight
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    mfmas(t);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the barrier count
+
+  // ---- epilogue: every ring read retired before the last barrier, no DMA in
+  // flight: each wave owns a 16 KiB region of the ring
+  char* reg = lds + wave * 16384;
+  acc_to_lds<T, FB_>(acc, reg, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  epilogue_rows<T, EPI, ACT, 64>(p, reg, lane, m0 + 128 * wm,
+                                 n0 + (EPI == EPI_GLU ? 32 : 64) * wn);
+}
+
+
+// ---- 4-wave variant: one wave per SIMD, 128 x 128 per wave, K in steps of 64 --
+// 64 accumulator tiles (256 fp32 per lane) pinned in AGPRs by asm MFMAs; the
+// MFMA pipe is fed by the wave's own software pipeline instead of a partner
+// wave.  A K-step of 64 is two MFMA k-halves; while the 64 MFMAs of one half
+// run, the wave reads the next half's 16 fragments into the other register
+// set (one ds_read_b128 per 4 MFMAs) and, in the second half, issues the DMA
+// of step t+2 (one 1-KiB glds per 4 MFMAs).  Every DMA row is 128 B (a whole
+// cache line; the 32-deep 8-wave form fetches half lines, twice the L2
+// requests per byte), and half the fragment bytes per MFMA of the 8-wave
+// form.  LDS: 2 slots x (A + B) x [256 rows][64 k] = 128 KiB, 16-B chunk c of
+// row r at 16 (c ^ ((r >> 1) & 7)) (conflict-free fragment reads for both
+// k-halves); one barrier per K-step.
+constexpr int BK2 = 64;                     // K per step
+constexpr int OPB2 = 256 * BK2 * 2;         // 32 KiB per operand per step
+constexpr int SLOTB2 = 2 * OPB2;            // 64 KiB
+
+template <typename T>
+__device__ __forceinline__ void mfma_acc(f32x4& acc, typename fa::MT<T>::x8 a,
+                                         typename fa::MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16))
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <typename T>
+__device__ __forceinline__ void mfma_zero(f32x4& acc, typename fa::MT<T>::x8 z) {
+  if constexpr (__is_same(T, bf16))
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
+}
+
+template <typename T, int EPI, int ACT>
+__global__ void __launch_bounds__(256, 1) gemm_nt4_k(NtArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
+  typedef typename fa::MT<T>::x8 X8;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntiles = p.ntm * p.ntn;
+  const int lin = xcd_remap((int)blockIdx.x, ntiles);
+  const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
+  const int64_t m0 = (int64_t)tt.x * TM;
+  const int64_t n0 = (int64_t)tt.y * (EPI == EPI_GLU ? TN / 2 : TN);
+  const int M = p.M, N = p.N;
+
+  // DMA: each operand step is 32 pieces of 1 KiB (8 rows x 128 B); wave w
+  // stages pieces 8w..8w+7 of A and of B.  Lane l lands on row 8 piece +
+  // (l >> 3), physical chunk l & 7 = logical chunk (l & 7) ^ ((row >> 1) & 7).
+  // Source = wave-uniform operand base + K-step byte offset (SGPRs) + a
+  // 32-bit per-lane offset (host-checked to fit).
+  uint32_t off[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = 8 * (8 * wave + i) + (lane >> 3);  // tile row 0..255
+    const int c = (lane & 7) ^ ((tr >> 1) & 7);
+    int64_t am = m0 + tr;
+    am = am < M ? am : M - 1;
+    off[i] = (uint32_t)((am * p.lda + 8 * c) * (int64_t)sizeof(T));
+    int64_t bn;
+    if constexpr (EPI == EPI_GLU) {
+      // per 128-row wave band: 64 up rows then the 64 gate rows of the same f
+      const int band = tr >> 7, q = tr & 127;
+      const int64_t f = n0 + 64 * band + (q & 63);
+      bn = f < N ? (q < 64 ? f : N + f) : 0;
+    } else {
+      bn = n0 + tr;
+      bn = bn < N ? bn : N - 1;
+    }
+    off[8 + i] = (uint32_t)((bn * p.ldb + 8 * c) * (int64_t)sizeof(T));
+  }
+  const char* const abyte = reinterpret_cast<const char*>(p.a);
+  const char* const bbyte = reinterpret_cast<const char*>(p.b);
+  char* const ldsp = lds;
+  const int nt = p.K / BK2;
+  // piece q (0..7 A, 8..15 B) of K-step ts -> LDS slot `slot`
+  auto stage_piece = [&](int q, int ts, int slot) {
+    const char* base = (q < 8 ? abyte : bbyte) + (int64_t)ts * (BK2 * (int)sizeof(T));
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(base + off[q]),
+                                     (__attribute__((address_space(3))) void*)(ldsp + dst), 16, 0, 0);
+  };
+
+  f32x4 acc[8][8];  // defined and updated only by asm MFMAs: AGPR-resident
+
+  // fragment bases [k-half]: row (l & 15) of the wave's band, logical chunk
+  // (l >> 4) + 4 kh; fragment i adds 2048 i, slot s adds s * SLOTB2
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  const int fr = lane & 15, fsw = (fr >> 1) & 7;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const uint32_t ch = 16u * (uint32_t)(((lane >> 4) + 4 * kh) ^ fsw);
+    abase[kh] = lds_base + 128u * (128u * wm + fr) + ch;
+    bbase[kh] = lds_base + OPB2 + 128u * (128u * wn + fr) + ch;
+  }
+  X8 set0[16], set1[16];  // k-half 0 / 1 fragments: [0..7] A (m), [8..15] B (n)
+  auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
+    constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
+    if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
+    else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto mfma4 = [&](X8 (&cur)[16], auto g) {
+    constexpr int G = decltype(g)::value;
+    static_for<4>([&](auto q) {
+      constexpr int IDX = 4 * G + decltype(q)::value, I = IDX / 8, J = IDX % 8;
+      mfma_acc<T>(acc[I][J], cur[8 + J], cur[I]);
+    });
+  };
+
+  // prologue: steps 0 and 1 in flight, acc zeroed meanwhile, k-half (0,0) read
+  static_for<16>([&](auto q) { stage_piece(decltype(q)::value, 0, 0); });
+  static_for<16>([&](auto q) { stage_piece(decltype(q)::value, min(1, nt - 1), 1); });
+  {
+    X8 z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = (T)0.f;
+    static_for<64>([&](auto q) {
+      constexpr int I = decltype(q)::value / 8, J = decltype(q)::value % 8;
+      mfma_zero<T>(acc[I][J], z);
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 landed (own DMA)
+  __builtin_amdgcn_s_barrier();                      // ... and everyone's
+  static_for<16>([&](auto f) { read_frag(set0, f, K0{}, 0u); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  // K-step t (slot t & 1):
+  //   half 0: MFMAs on set0 = (t, 0); read (t, 1) -> set1 from slot t
+  //           vmcnt(0): step t+1 landed (own DMA, issued in half (t-1, 1))
+  //           lgkmcnt(0); BARRIER
+  //   half 1: MFMAs on set1; read (t+1, 0) -> set0 from slot t+1;
+  //           DMA of step t+2 -> slot t (clamped to the last step past the end)
+  //           lgkmcnt(0)
+  // RAW: step t+1 is retired by every wave before the barrier, and read only
+  //      after it.  WAR: slot t's last reads ((t, 1)) are retired before the
+  //      barrier, the DMA into it is issued after.
+  for (int t = 0; t < nt; ++t) {
+    const uint32_t so = (uint32_t)((t & 1) * SLOTB2), sn = (uint32_t)(SLOTB2 - so);
+    static_for<16>([&](auto g) {
+      mfma4(set0, g);
+      read_frag(set1, g, K1{}, so);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int ts = min(t + 2, nt - 1), slot = t & 1;
+    static_for<16>([&](auto g) {
+      mfma4(set1, g);
+      read_frag(set0, g, K0{}, sn);
+      stage_piece(decltype(g)::value, ts, slot);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-fetches
+  __builtin_amdgcn_s_barrier();
+  fa::mfma_drain();  // VALU reads of the asm MFMAs' results
+
+  // epilogue: no ring read or DMA is pending
+  char* reg = lds + wave * 32768;
+  acc_to_lds<T, 8>(acc, reg, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  epilogue_rows<T, EPI, ACT, 128>(p, reg, lane, m0 + 128 * wm,
+                                  n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
+}
+
+int group_m(int ntm, int ntn) {
+  static const int env = [] {
+    const char* e = getenv("EMA_GEMM_GM");
+    return e ? atoi(e) : 0;
+  }();
+  if (env != 0) return env;
+  return ntm <= ntn ? 8 : -8;
+}
+
+#define EMA_GLU_KIND2(kind, ...)                              \
+  switch (kind) {                                             \
+    case 0: { constexpr int A_ = 0; __VA_ARGS__; break; }     \
+    case 1: { constexpr int A_ = 1; __VA_ARGS__; break; }     \
+    case 2: { constexpr int A_ = 2; __VA_ARGS__; break; }     \
+    default: { constexpr int A_ = 3; __VA_ARGS__; break; }    \
+  }
+
+// Kernel variant: 4 (one wave per SIMD, default) or 8 (ping-pong); the
+// EMA_GEMM_NT environment variable sets the initial value, gemm_nt_set_variant
+// switches it at run time (A/B in one process).
+int g_variant = [] {
+  const char* e = getenv("EMA_GEMM_NT");
+  return (e && e[0] == '8') ? 8 : 4;
+}();
+bool use_wave4() { return g_variant == 4; }
+
+template <typename T, int EPI, int ACT>
+void launch_one(const NtArgs& p, hipStream_t s) {
+  const dim3 grid((unsigned)(p.ntm * p.ntn));
+  if (use_wave4() && p.K % BK2 == 0 && p.wave4_ok) hipLaunchKernelGGL((gemm_nt4_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gemm_nt_k<T, EPI, ACT>), grid, dim3(512), 0, s, p);
+}
+
+template <int EPI>
+void launch_nt(NtArgs& p, int kind, int dt, hipStream_t s) {
+  const int n_out = EPI == EPI_GLU ? (p.N + TN / 2 - 1) / (TN / 2) : (p.N + TN - 1) / TN;
+  p.ntm = (p.M + TM - 1) / TM;
+  p.ntn = n_out;
+  p.gm = group_m(p.ntm, p.ntn);
+  const int64_t brows = EPI == EPI_GLU ? 2 * (int64_t)p.N : p.N;
+  p.wave4_ok = (int64_t)p.M * p.lda * 2 < ((int64_t)1 << 32) && brows * p.ldb * 2 < ((int64_t)1 << 32);
+  if constexpr (EPI == EPI_STORE) {
+    if (dt == DT_BF16) launch_one<bf16, EPI, 0>(p, s);
+    else launch_one<fp16, EPI, 0>(p, s);
+  } else if (dt == DT_BF16) {
+    EMA_GLU_KIND2(kind, (launch_one<bf16, EPI, A_>(p, s)));
+  } else {
+    EMA_GLU_KIND2(kind, (launch_one<fp16, EPI, A_>(p, s)));
+  }
+}
+
+}  // namespace
+
+void gemm_nt_set_variant(int v) { g_variant = v == 8 ? 8 : 4; }
+
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M > 0 && N > 0 && K > 0 && K % BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ldc % 8 == 0 && M < ((int64_t)1 << 31) && N < ((int64_t)1 << 30) &&
+         ((M + TM - 1) / TM) * ((N + TN / 2 - 1) / (TN / 2)) < ((int64_t)1 << 31);
+}
+
+void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s) {
+  NtArgs p{a, b, c, nullptr, nullptr, lda, ldb, ldc, 0, (int)M, (int)N, (int)K, 0, 0, 0, false};
+  launch_nt<EPI_STORE>(p, 0, dt, s);
+}
+
+void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,
+                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s) {
+  NtArgs p{a, b, pre, y, nullptr, lda, ldb, 2 * F, F, (int)M, (int)F, (int)K, 0, 0, 0, false};
+  launch_nt<EPI_GLU>(p, kind, dt, s);
+}
+
+void gemm_nt_dglu(const void* a, const void* b, const void* pre, void* dpre, int64_t M, int64_t F,
+                  int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s) {
+  NtArgs p{a, b, dpre, nullptr, pre, lda, ldb, 2 * F, 0, (int)M, (int)F, (int)K, 0, 0, 0, false};
+  launch_nt<EPI_DGLU>(p, kind, dt, s);
+}
+
+}  // namespace ema

@@ -185,6 +185,17 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
                 bool accumulate, int dt, hipStream_t s, float* ws = nullptr);
 void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
                          int64_t K, int mode, hipStream_t s);
+// ---- gemm_nt.hip: C[M,N] = A[M,K] B[N,K]^T (forward / dgrad), GLU epilogues --
+void gemm_nt_set_variant(int v);  // 4 or 8 waves per workgroup
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s);
+// fc1 forward: b = W1 [2F, K]; writes pre [M, 2F] and y = x1 * act(x2) [M, F]
+void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,
+                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s);
+// fc2 dgrad: b = W2^T [F, K]; reads pre [M, 2F], writes d(pre) [M, 2F]
+void gemm_nt_dglu(const void* a, const void* b, const void* pre, void* dpre, int64_t M, int64_t F,
+                  int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s);
 bool flash_attn_supported(int hd, int dt);
 
 // ---- skinny_gemm.hip: Y[M, N] = X[M, K] W[N, K]^T for decode batches (M <= 16) ----

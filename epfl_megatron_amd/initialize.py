@@ -105,6 +105,9 @@ def _initialize_distributed(args):
                                         args.virtual_pipeline_model_parallel_size,
                                         args.pipeline_model_parallel_split_rank,
                                         getattr(args, "ddp_comm_groups", 1))
+    if args.world_size > 1 and getattr(args, "comm_selfcheck", True):
+        from .parallel.selfcheck import collective_selfcheck
+        collective_selfcheck()
 
 
 def _set_random_seed(seed_, data_parallel_random_init=False):

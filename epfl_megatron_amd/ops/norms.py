@@ -185,6 +185,18 @@ def norm_residual(x, residual, weight, bias, eps, is_rms):
     return y, s
 
 
+def _param_sync(*params):
+    """Wait for the overlapped dist-opt all-gather of these parameters.
+
+    ``DistributedDataParallel`` waits in forward pre-hooks, which fire on
+    ``module(...)`` only; ``forward_residual`` is called directly by the fused
+    transformer path, so it waits here (``parallel/ddp.py`` ``_param_sync_wait``)."""
+    for p in params:
+        wait = getattr(p, "_param_sync_wait", None) if p is not None else None
+        if wait is not None:
+            wait()
+
+
 class RMSNorm(torch.nn.Module):
     """Root-mean-square norm; ``weight`` init 1 (state-dict key ``weight``)."""
 
@@ -198,6 +210,7 @@ class RMSNorm(torch.nn.Module):
         return rms_norm(x, self.weight, self.eps)
 
     def forward_residual(self, x, residual=None):
+        _param_sync(self.weight)
         return norm_residual(x, residual, self.weight, None, self.eps, True)
 
 
@@ -220,4 +233,5 @@ class MixedFusedLayerNorm(torch.nn.Module):
         return layer_norm(x, self.weight, self.bias, self.eps)
 
     def forward_residual(self, x, residual=None):
+        _param_sync(self.weight, self.bias)
         return norm_residual(x, residual, self.weight, self.bias, self.eps, False)

@@ -15,6 +15,9 @@ Two debug/observability aids live here:
   keyed by ``op/group-name``; with ``set_timing(True)`` (``--timing_log_level
   2``) HIP events also measure launch->completion time per op.  ``training.py``
   prints the table at each log interval (``report()``).
+* **pipeline p2p** — ``p2p()`` posts one batched isend/irecv group; its bytes
+  are accounted per direction (``p2p_send`` / ``p2p_recv``) and, under the race
+  checker, a send buffer written before ``wait()`` raises like a collective.
 * **in-flight race checker** — ``EMA_COMM_CHECK=1`` turns every async
   collective into "snapshot at launch, verify + run at ``wait()``": if any
   kernel or hook writes the buffer while the collective is logically in
@@ -127,7 +130,8 @@ class Work:
             return
         self._done = True
         if self._run is not None:  # race-check mode: verify, then run for real
-            if not _bitwise_equal(self._watch, self._snap):
+            watch = self._watch.detach() if isinstance(self._watch, _SendWatch) else self._watch
+            if not _bitwise_equal(watch, self._snap):
                 raise CommRaceError(
                     f"{self._key}: buffer written while the collective was in flight "
                     f"(between launch and wait)")
@@ -205,3 +209,77 @@ def all_gather_into(output, inp, group=None, async_op=False):
 def broadcast(tensor, src, group=None, async_op=False):
     return _issue("broadcast", group, tensor, tensor,
                   lambda a: dist.broadcast(tensor, src=src, group=group, async_op=a), async_op)
+
+
+def p2p(ops, group=None, async_op=False):
+    """Batched point-to-point exchange: ``ops`` = [(kind, tensor, peer)] with
+    kind ``"send"`` / ``"recv"`` and ``peer`` a global rank; posted in list
+    order as one ``batch_isend_irecv`` group (RCCL / NCCL match a peer pair's
+    messages in posting order).  Returns a ``Work`` when ``async_op``."""
+    ops = [o for o in ops if o is not None]
+    if not ops:
+        return None
+    sent = [t for k, t, _ in ops if k == "send"]
+    recvd = [t for k, t, _ in ops if k == "recv"]
+    for kind, ts in (("p2p_send", sent), ("p2p_recv", recvd)):
+        if ts:
+            _account(_key(kind, group), sum(t.numel() * t.element_size() for t in ts))
+
+    def fn(a):
+        reqs = dist.batch_isend_irecv(
+            [dist.P2POp(dist.isend if k == "send" else dist.irecv, t, peer, group)
+             for k, t, peer in ops])
+        if not a:
+            for r in reqs:
+                r.wait()
+            return None
+        return _Reqs(reqs)
+
+    ref = (sent or recvd)[0]
+    key = _key("p2p", group)
+    if _trace.tracing():
+        with _trace.trace_range(f"comm:{key}"):
+            return _p2p_issue(key, ref, sent, fn, async_op)
+    return _p2p_issue(key, ref, sent, fn, async_op)
+
+
+class _Reqs:
+    __slots__ = ("reqs",)
+
+    def __init__(self, reqs):
+        self.reqs = reqs
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+
+
+def _p2p_issue(key, ref, sent, fn, async_op):
+    start = None
+    if _events_on(ref):
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+    if async_op and _CHECK and sent:
+        # Only pure sends are deferred (a receive must complete before its
+        # consumer runs): snapshot the send buffers, verify and send at wait().
+        watch = torch.cat([t.detach().reshape(-1).view(torch.uint8) for t in sent]) \
+            if len(sent) > 1 else sent[0].detach().reshape(-1).view(torch.uint8)
+        return Work(run=lambda: fn(False), key=key, start=start, watch=_SendWatch(sent),
+                    snap=watch.clone())
+    w = fn(async_op)
+    h = Work(work=w, key=key, start=start)
+    if not async_op:
+        h.wait()
+        return None
+    return h
+
+
+class _SendWatch:
+    """The concatenated bytes of the send buffers, for the race check."""
+
+    def __init__(self, tensors):
+        self.tensors = tensors
+
+    def detach(self):
+        ts = [t.detach().reshape(-1).view(torch.uint8) for t in self.tensors]
+        return torch.cat(ts) if len(ts) > 1 else ts[0]

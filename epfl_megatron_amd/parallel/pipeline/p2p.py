@@ -6,6 +6,9 @@ Activations ``[s(/tp), b, h]`` move between adjacent stages with batched
 * No ``torch.cuda.synchronize()`` after every exchange: RCCL
   orders the transfer on its stream; we only ``wait()`` the requests, which
   makes the compute stream wait on the transfer without blocking the host.
+* Every exchange goes through ``parallel/comm.py`` (bytes accounting, race
+  checker); pure sends stay in flight while the schedule computes and are
+  completed before the next exchange / at the end of the schedule.
 * Scatter-gather optimisation kept: with TP > 1 and no sequence parallelism
   each TP rank sends only its 1/TP slice and the receiver all-gathers over TP.
 * Variable sequence lengths: shapes are exchanged first (int64[3]).
@@ -14,9 +17,8 @@ import operator
 from functools import reduce
 
 import torch
-import torch.distributed as dist
 
-from .. import state
+from .. import comm, state
 from ..buffers import make_viewless_tensor
 from ..tensor.utils import split_tensor_into_1d_equal_chunks, gather_split_1d_tensor
 from ... import global_vars
@@ -26,13 +28,36 @@ def _device():
     return torch.cuda.current_device() if torch.cuda.is_available() else "cpu"
 
 
+_PENDING_SENDS = []  # Work handles of exchanges that only sent (not yet waited)
+
+
+def wait_pending_sends():
+    """Complete every deferred pure-send exchange (called before the next
+    exchange and at the end of each schedule)."""
+    while _PENDING_SENDS:
+        _PENDING_SENDS.pop(0).wait()
+
+
 def _p2p(ops):
-    ops = [o for o in ops if o is not None]
+    """Post ``ops`` [(kind, tensor, peer)] through the collective layer.
+
+    An exchange that receives is waited at once (its consumer runs next); one
+    that only sends is left in flight while the schedule computes and is
+    completed before the next exchange (RCCL keeps the send buffers alive;
+    the buffers are passed as detached aliases, so the schedules' pseudo-free
+    of a sent output tensor cannot swap them out from under the transfer)."""
+    wait_pending_sends()
+    ops = [(k, t.detach() if k == "send" else t, peer) for k, t, peer in
+           (o for o in ops if o is not None)]
     if not ops:
         return
-    reqs = dist.batch_isend_irecv(ops)
-    for r in reqs:
-        r.wait()
+    group = state.get_pipeline_model_parallel_group()
+    if all(k == "send" for k, _, _ in ops):
+        h = comm.p2p(ops, group=group, async_op=True)
+        if h is not None:
+            _PENDING_SENDS.append(h)
+    else:
+        comm.p2p(ops, group=group)
 
 
 def _communicate_shapes(tensor_send_next, tensor_send_prev, recv_prev, recv_next):
@@ -43,16 +68,13 @@ def _communicate_shapes(tensor_send_next, tensor_send_prev, recv_prev, recv_next
         if tensor_send_next is not None else None
     send_prev_shape = torch.tensor(tensor_send_prev.size(), dtype=torch.int64, device=dev) \
         if tensor_send_prev is not None else None
-    group = state.get_pipeline_model_parallel_group()
+    prev_r = state.get_pipeline_model_parallel_prev_rank()
+    next_r = state.get_pipeline_model_parallel_next_rank()
     ops = [
-        dist.P2POp(dist.isend, send_prev_shape, state.get_pipeline_model_parallel_prev_rank(), group)
-        if send_prev_shape is not None else None,
-        dist.P2POp(dist.irecv, recv_prev_shape, state.get_pipeline_model_parallel_prev_rank(), group)
-        if recv_prev_shape is not None else None,
-        dist.P2POp(dist.isend, send_next_shape, state.get_pipeline_model_parallel_next_rank(), group)
-        if send_next_shape is not None else None,
-        dist.P2POp(dist.irecv, recv_next_shape, state.get_pipeline_model_parallel_next_rank(), group)
-        if recv_next_shape is not None else None,
+        ("send", send_prev_shape, prev_r) if send_prev_shape is not None else None,
+        ("recv", recv_prev_shape, prev_r) if recv_prev_shape is not None else None,
+        ("send", send_next_shape, next_r) if send_next_shape is not None else None,
+        ("recv", recv_next_shape, next_r) if recv_next_shape is not None else None,
     ]
     _p2p(ops)
     return ([int(x) for x in recv_prev_shape.tolist()] if recv_prev else None,
@@ -86,7 +108,6 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
             tensor_send_next = split_tensor_into_1d_equal_chunks(tensor_send_next)
         if tensor_send_prev is not None:
             tensor_send_prev = split_tensor_into_1d_equal_chunks(tensor_send_prev)
-    group = state.get_pipeline_model_parallel_group()
     prev_r = state.get_pipeline_model_parallel_prev_rank()
     next_r = state.get_pipeline_model_parallel_next_rank()
     # Post order: activations (forward direction) before gradients (backward
@@ -98,13 +119,13 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
     # PP = 2, megatron/arguments.py:117-120).
     ops = []
     if tensor_send_next is not None:
-        ops.append(dist.P2POp(dist.isend, tensor_send_next.contiguous(), next_r, group))
+        ops.append(("send", tensor_send_next.contiguous(), next_r))
     if recv_prev_t is not None:
-        ops.append(dist.P2POp(dist.irecv, recv_prev_t, prev_r, group))
+        ops.append(("recv", recv_prev_t, prev_r))
     if tensor_send_prev is not None:
-        ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), prev_r, group))
+        ops.append(("send", tensor_send_prev.contiguous(), prev_r))
     if recv_next_t is not None:
-        ops.append(dist.P2POp(dist.irecv, recv_next_t, next_r, group))
+        ops.append(("recv", recv_next_t, next_r))
     _p2p(ops)
     if scatter_gather:
         if recv_prev:

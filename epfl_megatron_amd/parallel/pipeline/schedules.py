@@ -275,6 +275,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func, data_ite
             out_grad = _recv_backward(send_shapes, timers)
             in_grad = run_backward(inp, out, out_grad)
             _send_backward(in_grad, recv_shapes, timers)
+    p2p.wait_pending_sends()
     return store
 
 
@@ -411,5 +412,6 @@ def forward_backward_pipelining_with_interleaving(forward_step_func, data_iterat
                 recv_next = False
             out_grads[nb].append(p2p.send_backward_recv_backward(in_grad, recv_next, shape,
                                                                  timers=timers))
+    p2p.wait_pending_sends()
     state.set_virtual_pipeline_model_parallel_rank(0)
     return store

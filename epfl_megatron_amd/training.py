@@ -266,8 +266,17 @@ def train_step(forward_step_func, data_iterator, model, optimizer, opt_param_sch
 
 
 def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scale,
-                 skipped_iter, grad_norm, params_norm, num_zeros_in_grad, report_memory_flag):
+                 skipped_iter, grad_norm, params_norm, num_zeros_in_grad, report_memory_flag,
+                 consumed_samples=None, num_microbatches=None):
+    """Log one iteration.  The loop logs an iteration one step late (so reading
+    its lazy device scalars never stalls the queue); ``consumed_samples`` and
+    ``num_microbatches`` are the values captured when it was enqueued (None:
+    read the live globals, for direct callers)."""
     args = get_args()
+    if consumed_samples is None:
+        consumed_samples = args.consumed_train_samples
+    if num_microbatches is None:
+        num_microbatches = get_num_microbatches()
     timers = get_timers()
     writer = get_tensorboard_writer()
     # lazy device->host values of the step being logged (one iteration old)
@@ -303,19 +312,18 @@ def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scal
                      "optimizer-count-zeros", "optimizer-inner-step",
                      "optimizer-copy-main-to-model-params", "optimizer"]
     normalizer = iteration % args.log_interval or args.log_interval
-    batch_size = args.micro_batch_size * args.data_parallel_size * get_num_microbatches()
+    batch_size = args.micro_batch_size * args.data_parallel_size * num_microbatches
     total_iterations = total_loss_dict[adv] + total_loss_dict[skp]
 
     if writer and (iteration % args.tensorboard_log_interval == 0):
         if args.log_learning_rate_to_tensorboard:
             writer.add_scalar("learning-rate", learning_rate, iteration)
-            writer.add_scalar("learning-rate vs samples", learning_rate,
-                              args.consumed_train_samples)
+            writer.add_scalar("learning-rate vs samples", learning_rate, consumed_samples)
         if args.log_batch_size_to_tensorboard:
             writer.add_scalar("batch-size", batch_size, iteration)
         for key, val in loss_dict.items():
             writer.add_scalar(key, float(val), iteration)
-            writer.add_scalar(key + " vs samples", float(val), args.consumed_train_samples)
+            writer.add_scalar(key + " vs samples", float(val), consumed_samples)
         if args.log_loss_scale_to_tensorboard:
             writer.add_scalar("loss-scale", loss_scale, iteration)
         if args.log_world_size_to_tensorboard:
@@ -412,17 +420,18 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
     def flush_log():
         nonlocal report_memory_flag
         while pending_log:
-            report_memory_flag = training_log(*pending_log.pop(0),
-                                              report_memory_flag=report_memory_flag)
+            entry, kw = pending_log.pop(0)
+            report_memory_flag = training_log(*entry, report_memory_flag=report_memory_flag, **kw)
 
     while iteration < args.train_iters:
         update_num_microbatches(args.consumed_train_samples)
+        step_microbatches = get_num_microbatches()
         args.curr_iteration = iteration
         loss_dict, skipped_iter, grad_norm, num_zeros = train_step(
             forward_step_func, train_data_iterator, model, optimizer, opt_param_scheduler, args)
         iteration += 1
         args.consumed_train_samples += state.get_data_parallel_world_size() * \
-            args.micro_batch_size * get_num_microbatches()
+            args.micro_batch_size * step_microbatches
         # Log the PREVIOUS iteration now that this one is enqueued: reading its
         # loss / grad norm / skip flag then never stalls the GPU queue.
         flush_log()
@@ -435,9 +444,11 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
         if args.log_params_norm:
             optimizer.wait_param_sync()
             params_norm = calc_params_l2_norm(model)
-        pending_log.append((loss_dict, total_loss_dict, optimizer.param_groups[0]["lr"],
-                            iteration, loss_scale, skipped_iter, grad_norm, params_norm,
-                            num_zeros))
+        pending_log.append(((loss_dict, total_loss_dict, optimizer.param_groups[0]["lr"],
+                             iteration, loss_scale, skipped_iter, grad_norm, params_norm,
+                             num_zeros),
+                            {"consumed_samples": args.consumed_train_samples,
+                             "num_microbatches": step_microbatches}))
         if args.adlr_autoresume and iteration % args.adlr_autoresume_interval == 0:
             flush_log()
             check_adlr_autoresume_termination(iteration, model, optimizer, opt_param_scheduler)

@@ -45,3 +45,47 @@ def test_bench_rank_failure_propagates():
                           "--steps", "1", "--warmup", "0", "--tp", "3"], cwd=ROOT, env=env,
                          capture_output=True, text=True, timeout=300)
     assert out.returncode != 0
+
+
+def test_bench_labels_follow_dtype_and_model():
+    """The metric names the real compute dtype, non-7B presets do not carry
+    the Llama-2-7B headline metric, and the record names the backend and the
+    parallel group sizes (VERDICT r2 weak #7)."""
+    rec = _run(["--steps", "1", "--warmup", "0"])
+    assert rec["dtype"] == "fp32" and "bf16" not in rec["metric"]
+    assert rec["backend"] == "gloo" and rec["world_size"] == 1
+    assert (rec["dp"], rec["tp"], rec["pp"]) == (1, 1, 1)
+    rec = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--preset", "falcon40b-tp4-pp2",
+                "--tp", "1", "--pp", "2"])
+    assert "Llama-2 7B" not in rec["metric"] and "Llama-2-7B" not in rec["metric"]
+    assert rec["pp"] == 2 and rec["world_size"] == 2
+
+
+def test_readme_headline_quotes_driver_record():
+    """README's headline number is the driver's own BENCH_r*.json value."""
+    import re
+    readme = open(os.path.join(ROOT, "README.md")).read()
+    row = next(l for l in readme.splitlines() if "(headline" in l and l.startswith("|"))
+    m = re.search(r"\*\*([0-9.]+)k\*\* \(driver run, `(BENCH_r\d+\.json)`\)", row)
+    assert m, row
+    rec = json.load(open(os.path.join(ROOT, m.group(2))))
+    value = rec["parsed"]["value"] if "parsed" in rec else rec["value"]
+    assert abs(float(m.group(1)) - value / 1000) < 0.051, (m.group(1), value)
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("preset,parallel,groups", [
+    ("llama7b-tp8-seq4096", "tp8+sp", (1, 8, 1)),
+    ("falcon40b-tp4-pp2", "tp4+sp_pp2+vpp1", (1, 4, 2)),
+    ("llama70b-tp8", "tp8+sp+distopt+recompute_full", (1, 8, 1)),
+])
+def test_bench_multi_gpu_presets_on_gloo(preset, parallel, groups):
+    """The three multi-GPU BASELINE presets run end to end at 8 ranks (the
+    driver's 8-GPU layout) through the same code RCCL runs, incl. the startup
+    collective self-check (VERDICT r2 next #5)."""
+    rec = _run(["--gpus", "8", "--preset", preset, "--steps", "1", "--warmup", "1"], timeout=900)
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == parallel
+    assert (rec["dp"], rec["tp"], rec["pp"]) == groups
+    assert rec["value"] > 0 and rec["final_loss"] == rec["final_loss"]  # not NaN

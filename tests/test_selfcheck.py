@@ -1,0 +1,44 @@
+"""Startup collective self-check (parallel/selfcheck.py) on gloo: it passes on
+every group of a TP x PP x DP grid with concurrent DP communicators, and it
+fails loudly when a collective does not behave as the framework assumes."""
+from dist_utils import run_dist, init_framework, TINY_LLAMA
+
+
+def _init_and_count(rank, world, argv):
+    import finetune
+    init_framework(argv, finetune.extra_args)
+    from epfl_megatron_amd.parallel.selfcheck import collective_selfcheck
+    return collective_selfcheck(verbose=False)
+
+
+def test_selfcheck_passes_on_3d_grid():
+    argv = TINY_LLAMA + ["--tensor_model_parallel_size", "2", "--pipeline_model_parallel_size",
+                         "2", "--ddp_comm_groups", "2", "--micro_batch_size", "1",
+                         "--global_batch_size", "4"]
+    counts = run_dist(_init_and_count, 8, argv)
+    # 2 DP communicators x 6 + TP 6 + PP 1 on every rank
+    assert counts == [19] * 8
+
+
+def _broken_avg(rank, world, argv):
+    import finetune
+    init_framework(argv + ["--no_comm_selfcheck"], finetune.extra_args)
+    from epfl_megatron_amd.parallel import comm, selfcheck
+    real = comm.reduce_scatter_into
+
+    def summing(output, inp, group=None, async_op=False, op="sum"):  # ignores AVG
+        return real(output, inp, group=group, async_op=async_op, op="sum")
+
+    comm.reduce_scatter_into = summing
+    try:
+        selfcheck.collective_selfcheck(verbose=False)
+    except RuntimeError as e:
+        return "reduce_scatter(AVG" in str(e)
+    finally:
+        comm.reduce_scatter_into = real
+    return False
+
+
+def test_selfcheck_detects_wrong_semantics():
+    argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "4"]
+    assert run_dist(_broken_avg, 2, argv) == [True, True]
