@@ -27,8 +27,10 @@ Other BASELINE configs, one command each (need >= tp*pp GPUs):
     --preset llama7b-tp8-seq4096     Llama-2-7B, TP=8 (SP), seq 4096
     --preset falcon40b-tp4-pp2       Falcon-40B, TP=4 x PP=2 interleaved, 8 micro-batches
     --preset llama70b-tp8            Llama-2-70B, TP=8 (SP), full recompute, dist-opt
-1-GPU per-rank proxies of the TP configs (same per-rank GEMM / attention
-shapes via --kv_channels; NOT the BASELINE metric, labelled "proxy"):
+1-GPU per-rank proxies of the TP configs (TP rank 0 of the real model built by
+--simulated_tensor_parallel_size: per-rank GEMM / attention shapes, s/tp-row
+norms and residuals under SP, TP collectives looped back locally and reported
+with an analytic xGMI time; NOT the BASELINE metric, labelled "proxy"):
     --proxy llama7b-tp8 | llama70b-tp8 | falcon40b-tp4-pp2
 """
 import argparse
@@ -65,8 +67,10 @@ PRESETS = {
     "falcon40b-tp4-pp2": dict(model="falcon-40b", tp=4, pp=2, vpp_layers=10, seq=2048, mbs=2,
                               nmicro=8, sp=True),
     # config #5
+    # (the reference recomputes every layer; 288 GB per MI355X holds most or all
+    # of the activations: the memory model picks the recompute depth)
     "llama70b-tp8": dict(model="llama2-70b", tp=8, pp=1, seq=4096, mbs=2, nmicro=8, sp=True,
-                         recompute="full", dist_opt=True),
+                         recompute_budget_gb=260, dist_opt=True),
 }
 
 PROXIES = {  # one TP rank of a BASELINE config on one GPU
@@ -92,10 +96,14 @@ def _parse(argv=None):
     ap.add_argument("--vpp_layers", type=int, default=None,
                     help="layers per virtual pipeline stage (interleaved 1F1B)")
     ap.add_argument("--recompute", default=None, choices=["selective", "full"])
+    ap.add_argument("--recompute_budget_gb", type=float, default=None,
+                    help="recompute only what the memory model needs to fit this peak")
     ap.add_argument("--no_sp", action="store_true")
     ap.add_argument("--no_dist_opt", action="store_true")
     ap.add_argument("--bucket_mb", type=float, default=512.0)
     ap.add_argument("--data", default="cycle", choices=["cycle", "uniform"])
+    ap.add_argument("--xgmi_busbw_gbs", type=float, default=300.0,
+                    help="proxies: assumed ring bus bandwidth for the analytic TP comm time")
     ap.add_argument("--extra", default="", help="extra framework flags (space separated)")
     return ap.parse_args(argv)
 
@@ -145,24 +153,20 @@ def _resolve(a, world):
         proxy_tp = PROXIES[a.proxy][1]
     for k, v in (("model", a.model), ("seq", a.seq_len), ("mbs", a.micro_batch),
                  ("nmicro", a.num_micro), ("tp", a.tp), ("pp", a.pp),
-                 ("vpp_layers", a.vpp_layers), ("recompute", a.recompute)):
+                 ("vpp_layers", a.vpp_layers), ("recompute", a.recompute),
+                 ("recompute_budget_gb", a.recompute_budget_gb)):
         if v is not None:
             cfg[k] = v
     if a.no_sp:
         cfg["sp"] = False
     shape = dict(MODELS[cfg["model"]])
     if proxy_tp:
-        # one TP rank (and one PP stage) of the real model on one GPU
-        pp = cfg.get("pp", 1)
-        hd = shape["h"] // shape["nh"]
-        shape["L"] //= pp
-        shape["kv_channels"] = hd
-        shape["nh"] //= proxy_tp
-        shape["nkv"] = max(1, (shape["nkv"] or MODELS[cfg["model"]]["nh"]) // proxy_tp)
-        ffn = shape["ffn"] or 4 * shape["h"]
-        shape["ffn"] = ffn // proxy_tp
-        shape["vocab"] = -(-shape["vocab"] // proxy_tp)
-        cfg.update(tp=1, pp=1, sp=False, vpp_layers=None)
+        # one TP rank (and one PP stage) of the real model on one GPU: the
+        # framework builds TP rank 0 of a TP=proxy_tp model (sharded heads,
+        # FFN, vocab; s/tp-row norms / residuals under SP) and its TP
+        # collectives loop back locally (--simulated_tensor_parallel_size)
+        shape["L"] //= cfg.get("pp", 1)
+        cfg.update(sim_tp=proxy_tp, tp=1, pp=1, vpp_layers=None)
     return cfg, shape
 
 
@@ -202,7 +206,10 @@ def _framework_argv(a, cfg, shape, world, on_gpu):
         argv += ["--parallel_attn", "--model_name", "falcon"]
         if s.get("parallel_layernorm"):
             argv += ["--parallel_layernorm"]
-    if cfg.get("sp") and tp > 1:
+    sim_tp = cfg.get("sim_tp")
+    if sim_tp:
+        argv += ["--simulated_tensor_parallel_size", str(sim_tp)]
+    if cfg.get("sp") and (tp > 1 or sim_tp):
         argv += ["--sequence_parallel"]
     if cfg.get("vpp_layers") and pp > 1:
         argv += ["--num_layers_per_virtual_pipeline_stage", str(cfg["vpp_layers"])]
@@ -220,11 +227,38 @@ def _framework_argv(a, cfg, shape, world, on_gpu):
         argv += ["--recompute_granularity", rc]
         if rc == "full":
             argv += ["--recompute_method", "uniform", "--recompute_num_layers", "1"]
+    elif cfg.get("recompute_budget_gb"):
+        rc = f"budget{cfg['recompute_budget_gb']:g}gb"
+        argv += ["--recompute_memory_budget_gb", str(cfg["recompute_budget_gb"])]
     if a.extra:
         argv += a.extra.split()
     return argv, dict(tp=tp, pp=pp, dp=dp, gbs=gbs, mbs=mbs, nmicro=nmicro, seq=seq,
                       dist_opt=bool(dist_opt), vpp=cfg.get("vpp_layers") if pp > 1 else None,
-                      recompute=rc, sp=bool(cfg.get("sp") and tp > 1))
+                      recompute=rc, sp=bool(cfg.get("sp") and (tp > 1 or sim_tp)),
+                      sim_tp=sim_tp)
+
+
+def _proxy_comm(rep, n, steps, ms_step, busbw_gbs):
+    """Per-step TP traffic of the simulated rank (from the comm accounting)
+    and an analytic xGMI time for it: ring all-gather / reduce-scatter move
+    (n-1)/n of the full buffer per rank, all-reduce twice that, at a bus
+    bandwidth of ``busbw_gbs`` GB/s (an assumption, stated in the record)."""
+    tp_bytes, wire = 0.0, 0.0
+    detail = {}
+    for key, (cnt, nbytes, _) in rep.items():
+        op, _, grp = key.partition("/")
+        if grp != "tp":
+            continue
+        f = (n - 1) / n * (2.0 if op == "all_reduce" else 1.0)
+        tp_bytes += nbytes
+        wire += nbytes * f
+        detail[op] = {"calls_per_step": cnt / steps, "MiB_per_step": round(nbytes / steps / 2**20, 1)}
+    ms = wire / steps / (busbw_gbs * 1e9) * 1e3
+    return {"proxy_tp_collectives": detail,
+            "proxy_tp_wire_MiB_per_step": round(wire / steps / 2**20, 1),
+            "proxy_xgmi_busbw_GBs_assumed": busbw_gbs,
+            "proxy_tp_comm_ms_per_step_analytic": round(ms, 2),
+            "proxy_ms_per_step_if_comm_not_overlapped": round(ms_step + ms, 2)}
 
 
 def _label(cfg, shape, a):
@@ -258,8 +292,8 @@ def main(argv=None):
         shape = dict(MODELS["tiny"], family=fam["family"],
                      parallel_layernorm=fam.get("parallel_layernorm", False))
         if fam["family"] == "falcon":
-            shape.update(ffn=None, nkv=max(2, cfg.get("tp", 1)))
-        if cfg.get("tp", 1) > 1 or cfg.get("pp", 1) > 1:
+            shape.update(ffn=None, nkv=max(2, cfg.get("tp", 1), cfg.get("sim_tp") or 1))
+        if cfg.get("tp", 1) > 1 or cfg.get("pp", 1) > 1 or cfg.get("sim_tp"):
             shape["nh"] = 8
         shape["L"] = max(shape["L"], 2 * cfg.get("pp", 1))
         if cfg.get("vpp_layers"):
@@ -303,9 +337,11 @@ def main(argv=None):
             losses.append(out[0]["lm loss"])
         return out
 
+    from epfl_megatron_amd.parallel import comm
     for _ in range(a.warmup):
         step()
     sync()
+    comm.report(reset=True)
     if on_gpu:
         torch.cuda.reset_peak_memory_stats()
     t0 = time.perf_counter()
@@ -313,6 +349,7 @@ def main(argv=None):
         step()
     sync()
     dt = time.perf_counter() - t0
+    comm_rep = comm.report(reset=True)
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank defines the step time
@@ -330,11 +367,15 @@ def main(argv=None):
     optimizer.resolve_pending()
     tokens = par["gbs"] * par["seq"] * a.steps
     tok_s = tokens / dt
-    per_gpu = tok_s / world
+    # a simulated TP rank processes every token of its TP group at 1/tp of the
+    # FLOPs: per-GPU rate of the real configuration = group rate / tp
+    per_gpu = tok_s / world / (par["sim_tp"] or 1)
     fpt = flops_per_token(args)
     mfu = per_gpu * fpt / (args.peak_tflops * 1e12)
     if dist.get_rank() == 0:
         parallel = f"dp{par['dp']}"
+        if par["sim_tp"]:
+            parallel = f"proxy-tp{par['sim_tp']}" + ("+sp" if par["sp"] else "")
         if par["tp"] > 1:
             parallel = f"tp{par['tp']}" + ("+sp" if par["sp"] else "") + \
                 (f"_dp{par['dp']}" if par["dp"] > 1 else "")
@@ -348,7 +389,8 @@ def main(argv=None):
         dtype = "bf16" if on_gpu else "fp32"
         if a.proxy:
             metric = (f"PROXY (1 GPU = one TP rank of {a.proxy}; not the BASELINE metric): "
-                      f"per-rank tokens/s, {dtype}")
+                      f"tokens/s of the TP group this rank belongs to, {dtype} "
+                      "(per-GPU = value / tp in 'tokens_per_sec_per_gpu')")
             label = f"{label} [{a.proxy} per-rank proxy]"
         elif cfg["model"] == "llama2-7b":
             metric = (f"{BASELINE_METRIC} [{label} {dtype} training; value = tokens/s aggregate "
@@ -386,7 +428,17 @@ def main(argv=None):
             "backend": dist.get_backend(),
             "world_size": world,
             "dp": par["dp"], "tp": par["tp"], "pp": par["pp"],
+            "recompute": {"granularity": args.recompute_granularity,
+                          "method": args.recompute_method,
+                          "layers": (args.recompute_num_layers
+                                     if args.recompute_granularity == "full" else 0),
+                          "estimated_peak_gb": (round(args.recompute_estimate_gb, 1)
+                                                if getattr(args, "recompute_estimate_gb", None)
+                                                else None)},
         }
+        if a.proxy:
+            rec.update(_proxy_comm(comm_rep, par["sim_tp"], a.steps, 1000.0 * dt / a.steps,
+                                   a.xgmi_busbw_gbs))
         print(json.dumps(rec), flush=True)
     else:
         rec = None

@@ -132,6 +132,10 @@ FLAG_TABLE = {
         _flag("--distribute_saved_activations", action="store_true"),
         _flag("--recompute_method", type=str, default=None, choices=["uniform", "block"]),
         _flag("--recompute_num_layers", type=int, default=1),
+        _flag("--recompute_memory_budget_gb", type=float, default=None,
+              help="MI355X: recompute (block method) only as many layers per pipeline "
+                   "stage as needed for the estimated per-GPU peak to fit this many GB "
+                   "(utils/memory_model.py); 0 recomputed layers disables recompute"),
         _flag("--train_iters", type=int, default=None),
         _flag("--train_samples", type=int, default=None),
         _flag("--log_interval", type=int, default=100),
@@ -220,6 +224,13 @@ FLAG_TABLE = {
         # MI355X additions: bucketed, overlapped DP reduction sized for xGMI.
         _flag("--ddp_bucket_size_mb", type=float, default=256.0,
               help="fp32 gradient bucket size (MiB) for the overlapped DP reduction"),
+        _flag("--simulated_tensor_parallel_size", type=int, default=None,
+              help="MI355X per-rank proxy: build and run ONE tensor-parallel rank of a "
+                   "TP=N model in this process (sharded weights, heads, vocab and, with "
+                   "--sequence_parallel, s/N-row norms / residuals / dropout). TP "
+                   "collectives become local loopbacks (all-gather replicates the shard, "
+                   "reduce-scatter takes the mean of the N chunks) that are accounted in "
+                   "the comm table with the bytes a real rank would send"),
         _flag("--ddp_comm_groups", type=int, default=1,
               help="communicators over the DP ranks; DDP buckets are issued round-robin "
                    "on them so several reduce concurrently (one RCCL stream each)"),
@@ -532,13 +543,19 @@ def _derive_recompute_and_parallel_features(args):
     if not args.parallel_attn:
         _require(not args.parallel_layernorm,
                  "parallel_layernorm only implemented with parallel_attention")
-    if args.tensor_model_parallel_size == 1:
+    sim_tp = getattr(args, "simulated_tensor_parallel_size", None)
+    if sim_tp:
+        _require(args.tensor_model_parallel_size == 1 and args.pipeline_model_parallel_size == 1
+                 and args.world_size == 1,
+                 "--simulated_tensor_parallel_size runs one rank of a TP model in a single "
+                 "process (world size 1, no real TP / PP)")
+    if args.tensor_model_parallel_size == 1 and not (sim_tp and sim_tp > 1):
         args.sequence_parallel = False
     if args.sequence_parallel:
         args.async_tensor_model_parallel_allreduce = False
     # Reference defect D17: the GQA view silently breaks when KV heads do not
     # split evenly over TP ranks; we check it explicitly.
-    if args.num_attention_heads_kv % args.tensor_model_parallel_size != 0:
+    if args.num_attention_heads_kv % (sim_tp or args.tensor_model_parallel_size) != 0:
         raise AssertionError("num_attention_heads_kv must be divisible by "
                              "tensor_model_parallel_size")
 

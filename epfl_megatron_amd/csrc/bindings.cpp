@@ -740,29 +740,56 @@ bool gemm_nt_supported(const at::Tensor& a, const at::Tensor& b) {
          ema::gemm_nt_supported(a.size(0), b.size(0), a.size(1), a.stride(0), b.stride(0), b.size(0));
 }
 
-// c[M,N] = a[M,K] b[N,K]^T (c allocated unless given)
-at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::Tensor> out) {
+// Row-group remap from Python: (rows, stride, offset) or rows == 0.  The host
+// checks that every physical row of the remapped logical rows [0, M) lies in
+// [0, phys_rows) BEFORE launching.
+ema::RowMap row_map(const std::vector<int64_t>& m, int64_t M, int64_t phys_rows, const char* what) {
+  ema::RowMap r;
+  if (m.empty() || m[0] == 0) {
+    TORCH_CHECK(M <= phys_rows, what, ": ", M, " logical rows but ", phys_rows, " physical");
+    return r;
+  }
+  TORCH_CHECK(m.size() == 3 && m[0] > 0 && m[1] >= m[0] && m[2] >= 0 && m[0] < (1LL << 31) &&
+              M < (1LL << 31), what, ": row map must be (rows > 0, stride >= rows, offset >= 0)");
+  r.rows = (int)m[0];
+  r.stride = m[1];
+  r.offset = m[2];
+  const int64_t last = ((M - 1) / m[0]) * m[1] + m[2] + (M - 1) % m[0];
+  TORCH_CHECK(m[2] + std::min<int64_t>(m[0], M) - 1 <= last && last < phys_rows, what,
+              ": remapped rows exceed the operand (last row ", last, ", ", phys_rows, " rows)");
+  return r;
+}
+
+// c[M,N] = a[M,K] b[N,K]^T (c allocated unless given).  a_map: logical A row
+// q is row map(q) of `a` (M = m if given, else a.size(0)); c_map: output row q
+// goes to row map(q) of `out`.
+at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::Tensor> out,
+                   std::vector<int64_t> a_map, std::vector<int64_t> c_map, int64_t m) {
   check_gpu(a, "a");
   check_rows(a, "a");
   check_rows(b, "b");
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_nt: a/b dtype mismatch");
   const int dt = dtype_code(a);
   TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "gemm_nt: bf16/fp16 only");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  const int64_t M = m > 0 ? m : a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm_nt: reduction dims differ");
+  const ema::RowMap am = row_map(a_map, M, a.size(0), "gemm_nt a_map");
   at::Tensor c = out.has_value() ? *out : at::empty({M, N}, a.options());
   check_rows(c, "c");
-  TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.scalar_type() == a.scalar_type(),
-              "gemm_nt: bad output");
+  TORCH_CHECK(c.size(1) == N && c.scalar_type() == a.scalar_type(), "gemm_nt: bad output");
+  const ema::RowMap cm = row_map(c_map, M, c.size(0), "gemm_nt c_map");
   TORCH_CHECK(ema::gemm_nt_supported(M, N, K, a.stride(0), b.stride(0), c.stride(0)),
               "gemm_nt: unsupported shape (K % 32, N % 8)");
   ema::gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0), b.stride(0),
-               c.stride(0), dt, cur_stream());
+               c.stride(0), dt, cur_stream(), am, cm);
   return c;
 }
 
-// fc1 forward with the GLU fused: returns (pre [M, 2F], y [M, F])
-std::vector<at::Tensor> gemm_nt_glu(const at::Tensor& a, const at::Tensor& w1, int64_t kind) {
+// fc1 forward with the GLU fused: returns (pre [M, 2F], y [M, F]); with
+// c_map the rows go to the given pre / y through the map
+std::vector<at::Tensor> gemm_nt_glu(const at::Tensor& a, const at::Tensor& w1, int64_t kind,
+                                    c10::optional<at::Tensor> pre_out,
+                                    c10::optional<at::Tensor> y_out, std::vector<int64_t> c_map) {
   check_gpu(a, "a");
   check_rows(a, "a");
   check_rows(w1, "w1");
@@ -773,10 +800,18 @@ std::vector<at::Tensor> gemm_nt_glu(const at::Tensor& a, const at::Tensor& w1, i
   TORCH_CHECK(w1.size(1) == K && w1.size(0) == 2 * F, "gemm_nt_glu: w1 must be [2F, K]");
   TORCH_CHECK(ema::gemm_nt_supported(M, F, K, a.stride(0), w1.stride(0), 2 * F),
               "gemm_nt_glu: unsupported shape (K % 32, F % 8)");
-  auto pre = at::empty({M, 2 * F}, a.options());
-  auto y = at::empty({M, F}, a.options());
+  TORCH_CHECK(pre_out.has_value() == y_out.has_value(), "gemm_nt_glu: give both outputs or none");
+  auto pre = pre_out.has_value() ? *pre_out : at::empty({M, 2 * F}, a.options());
+  auto y = y_out.has_value() ? *y_out : at::empty({M, F}, a.options());
+  TORCH_CHECK(pre.is_contiguous() && y.is_contiguous() && pre.dim() == 2 && y.dim() == 2 &&
+              pre.size(1) == 2 * F && y.size(1) == F && pre.size(0) == y.size(0) &&
+              pre.scalar_type() == a.scalar_type() && y.scalar_type() == a.scalar_type(),
+              "gemm_nt_glu: outputs must be contiguous [R, 2F] and [R, F] of the operand dtype");
+  check_vec_aligned(pre, "pre");
+  check_vec_aligned(y, "y");
+  const ema::RowMap cm = row_map(c_map, M, pre.size(0), "gemm_nt_glu c_map");
   ema::gemm_nt_glu(a.data_ptr(), w1.data_ptr(), pre.data_ptr(), y.data_ptr(), M, F, K,
-                   a.stride(0), w1.stride(0), (int)kind, dt, cur_stream());
+                   a.stride(0), w1.stride(0), (int)kind, dt, cur_stream(), cm);
   return {pre, y};
 }
 
@@ -835,10 +870,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.def("wgrad_plan", &wgrad_plan);
-  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none(),
+        py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},
+        py::arg("m") = 0);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_set_variant", &ema::gemm_nt_set_variant);
-  m.def("gemm_nt_glu", &gemm_nt_glu);
+  m.def("gemm_nt_glu", &gemm_nt_glu, py::arg("a"), py::arg("w1"), py::arg("kind"),
+        py::arg("pre") = py::none(), py::arg("y") = py::none(),
+        py::arg("c_map") = std::vector<int64_t>{});
   m.def("gemm_nt_dglu", &gemm_nt_dglu);
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),

@@ -48,6 +48,10 @@
 //     an 8 (m) x 4 (n) block, sharing A and B panels in its L2.
 // Shapes: K % 32 == 0, N % 8 == 0 (F % 8 for the GLU forms), 16-B aligned rows;
 // ragged M and N tails are clamped on load and masked on store.
+// Row-group remap (RowMap, STORE / GLU): A rows may be read from, and C rows
+// written to, a strided set of row groups of a larger matrix — one chunk of
+// the sequence-parallel all-gather / reduce-scatter pipeline
+// (parallel/tensor/layers.py) runs as one launch without a copy.
 #include <cstdlib>
 
 #include "act_math.h"
@@ -115,7 +119,15 @@ struct NtArgs {
   int M, N, K;        // EPI_GLU / EPI_DGLU: N = F
   int ntm, ntn, gm;
   bool wave4_ok;      // 32-bit per-lane DMA offsets fit (the 4-wave kernel)
+  RowMap am, cm;      // row-group remap of A rows (loads) and C rows (stores)
 };
+
+// logical row q -> physical row (RowMap in kernels.h); q < 2^31
+__device__ __forceinline__ int64_t map_row(int64_t q, const RowMap& m) {
+  if (m.rows == 0) return q;
+  const uint32_t g = (uint32_t)q / (uint32_t)m.rows;
+  return (int64_t)g * m.stride + m.offset + (int64_t)((uint32_t)q - g * (uint32_t)m.rows);
+}
 
 
 // ---- epilogue (both kernels) ------------------------------------------------
@@ -168,9 +180,10 @@ __device__ __forceinline__ void epilogue_rows(const NtArgs& p, const char* reg, 
       for (int e = 0; e < V::N; ++e) o.v[e] = from_f<T>(to_f(x1.v[e]) * act<ACT>(to_f(x2.v[e])));
       const int64_t gm = gm0 + row;
       if (fok && gm < M) {
-        st16(pre + gm * p.ldc + f, x1);
-        st16(pre + gm * p.ldc + N + f, x2);
-        st16(y + gm * p.ldy + f, o);
+        const int64_t pr = map_row(gm, p.cm);
+        st16(pre + pr * p.ldc + f, x1);
+        st16(pre + pr * p.ldc + N + f, x2);
+        st16(y + pr * p.ldy + f, o);
       }
     }
   } else {
@@ -185,7 +198,7 @@ __device__ __forceinline__ void epilogue_rows(const NtArgs& p, const char* reg, 
         const int row = RPI * it + lane / LPR;
         const V v = unit(row, u);
         const int64_t gm = gm0 + row;
-        if (nok && gm < M) st16(c + gm * p.ldc + gn, v);
+        if (nok && gm < M) st16(c + map_row(gm, p.cm) * p.ldc + gn, v);
       }
     } else {
       // d(pre) = [g * act(x2), g * x1 * act'(x2)], g = dAct rounded to T
@@ -250,7 +263,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_k(NtArgs p) {
     for (int i = 0; i < 2; ++i) {
       const int tr = 16 * (2 * wave + i) + (lane >> 2);  // tile row 0..255
       int64_t am = m0 + tr;
-      am = am < M ? am : M - 1;
+      am = map_row(am < M ? am : M - 1, p.am);
       asrc[i] = reinterpret_cast<const T*>(p.a) + am * p.lda + 8 * c;
       int64_t bn;
       if constexpr (EPI == EPI_GLU) {
@@ -424,7 +437,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt4_k(NtArgs p) {
     const int tr = 8 * (8 * wave + i) + (lane >> 3);  // tile row 0..255
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
     int64_t am = m0 + tr;
-    am = am < M ? am : M - 1;
+    am = map_row(am < M ? am : M - 1, p.am);
     off[i] = (uint32_t)((am * p.lda + 8 * c) * (int64_t)sizeof(T));
     int64_t bn;
     if constexpr (EPI == EPI_GLU) {
@@ -581,7 +594,10 @@ void launch_nt(NtArgs& p, int kind, int dt, hipStream_t s) {
   p.ntn = n_out;
   p.gm = group_m(p.ntm, p.ntn);
   const int64_t brows = EPI == EPI_GLU ? 2 * (int64_t)p.N : p.N;
-  p.wave4_ok = (int64_t)p.M * p.lda * 2 < ((int64_t)1 << 32) && brows * p.ldb * 2 < ((int64_t)1 << 32);
+  // highest A row read (through the remap: groups are increasing in q)
+  const int64_t arows = p.am.rows == 0 ? p.M
+      : ((int64_t)(p.M - 1) / p.am.rows) * p.am.stride + p.am.offset + (p.M - 1) % p.am.rows + 1;
+  p.wave4_ok = arows * p.lda * 2 < ((int64_t)1 << 32) && brows * p.ldb * 2 < ((int64_t)1 << 32);
   if constexpr (EPI == EPI_STORE) {
     if (dt == DT_BF16) launch_one<bf16, EPI, 0>(p, s);
     else launch_one<fp16, EPI, 0>(p, s);
@@ -603,20 +619,24 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
 }
 
 void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
-             int64_t ldb, int64_t ldc, int dt, hipStream_t s) {
-  NtArgs p{a, b, c, nullptr, nullptr, lda, ldb, ldc, 0, (int)M, (int)N, (int)K, 0, 0, 0, false};
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap, RowMap cmap) {
+  NtArgs p{a, b, c, nullptr, nullptr, lda, ldb, ldc, 0, (int)M, (int)N, (int)K, 0, 0, 0, false,
+           amap, cmap};
   launch_nt<EPI_STORE>(p, 0, dt, s);
 }
 
 void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,
-                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s) {
-  NtArgs p{a, b, pre, y, nullptr, lda, ldb, 2 * F, F, (int)M, (int)F, (int)K, 0, 0, 0, false};
+                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s,
+                 RowMap cmap) {
+  NtArgs p{a, b, pre, y, nullptr, lda, ldb, 2 * F, F, (int)M, (int)F, (int)K, 0, 0, 0, false,
+           RowMap{}, cmap};
   launch_nt<EPI_GLU>(p, kind, dt, s);
 }
 
 void gemm_nt_dglu(const void* a, const void* b, const void* pre, void* dpre, int64_t M, int64_t F,
                   int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s) {
-  NtArgs p{a, b, dpre, nullptr, pre, lda, ldb, 2 * F, 0, (int)M, (int)F, (int)K, 0, 0, 0, false};
+  NtArgs p{a, b, dpre, nullptr, pre, lda, ldb, 2 * F, 0, (int)M, (int)F, (int)K, 0, 0, 0, false,
+           RowMap{}, RowMap{}};
   launch_nt<EPI_DGLU>(p, kind, dt, s);
 }
 

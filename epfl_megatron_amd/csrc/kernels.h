@@ -188,11 +188,20 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
 // ---- gemm_nt.hip: C[M,N] = A[M,K] B[N,K]^T (forward / dgrad), GLU epilogues --
 void gemm_nt_set_variant(int v);  // 4 or 8 waves per workgroup
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+// Row-group remap of an operand's rows (the chunked TP all-gather / reduce-
+// scatter overlap): logical row q lives at physical row
+//   (q / rows) * stride + offset + q % rows        (rows == 0: identity)
+struct RowMap {
+  int rows = 0;
+  int64_t stride = 0, offset = 0;
+};
 void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
-             int64_t ldb, int64_t ldc, int dt, hipStream_t s);
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap = {}, RowMap cmap = {});
 // fc1 forward: b = W1 [2F, K]; writes pre [M, 2F] and y = x1 * act(x2) [M, F]
+// (rows of both outputs through cmap)
 void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,
-                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s);
+                 int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s,
+                 RowMap cmap = {});
 // fc2 dgrad: b = W2^T [F, K]; reads pre [M, 2F], writes d(pre) [M, 2F]
 void gemm_nt_dglu(const void* a, const void* b, const void* pre, void* dpre, int64_t M, int64_t F,
                   int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s);

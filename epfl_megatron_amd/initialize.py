@@ -33,6 +33,8 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
         load_args_from_checkpoint(args)
     validate_args(args, args_defaults)
     global_vars.set_global_variables(args)
+    if getattr(args, "recompute_memory_budget_gb", None):
+        resolve_recompute_budget(args)
     _initialize_distributed(args)
     _set_random_seed(args.seed, args.data_parallel_random_init)
     if args.rank == 0:
@@ -105,9 +107,41 @@ def _initialize_distributed(args):
                                         args.virtual_pipeline_model_parallel_size,
                                         args.pipeline_model_parallel_split_rank,
                                         getattr(args, "ddp_comm_groups", 1))
+    sim_tp = getattr(args, "simulated_tensor_parallel_size", None)
+    if sim_tp and sim_tp > 1:
+        # one rank (rank 0) of a TP=sim_tp model; TP collectives loop back locally
+        from .parallel import comm
+        state.set_tensor_model_parallel_world_size(sim_tp)
+        state.set_tensor_model_parallel_rank(0)
+        comm.set_loopback(state.get_tensor_model_parallel_group(), sim_tp)
     if args.world_size > 1 and getattr(args, "comm_selfcheck", True):
         from .parallel.selfcheck import collective_selfcheck
         collective_selfcheck()
+
+
+def resolve_recompute_budget(args):
+    """--recompute_memory_budget_gb: pick the block-recompute layer count from
+    the memory model (needs the padded vocab, so it runs after the tokenizer)."""
+    from .utils import memory_model as mm
+    pp = args.pipeline_model_parallel_size
+    layers = args.num_layers // pp
+    n_params = mm.params_per_rank(args)
+    n = mm.auto_recompute_layers(args, n_params, layers, args.recompute_memory_budget_gb,
+                                 in_flight=pp)
+    est = mm.estimate(args, n_params, layers, n, in_flight=pp) / mm.GB
+    if n == 0:
+        args.recompute_granularity = None
+        args.recompute_method = None
+        args.distribute_saved_activations = False
+    else:
+        args.recompute_granularity = "full"
+        args.recompute_method = "block"
+        args.recompute_num_layers = n
+    args.recompute_estimate_gb = est
+    if args.rank == 0:
+        print(f"> recompute budget {args.recompute_memory_budget_gb:.0f} GB: {n} of {layers} "
+              f"layers per stage recomputed (estimated peak {est:.1f} GB)", flush=True)
+    return n
 
 
 def _set_random_seed(seed_, data_parallel_random_init=False):

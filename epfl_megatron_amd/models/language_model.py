@@ -207,7 +207,7 @@ class TransformerLanguageModel(MegatronModule):
             self._lm_key = "lm_head"
             start, end = tp.VocabUtility.vocab_range_from_global_vocab_size(
                 args.padded_vocab_size, state.get_tensor_model_parallel_rank(),
-                args.tensor_model_parallel_size)
+                state.get_tensor_model_parallel_world_size())
             rows = end - start
             cpu_init = bool(args.use_cpu_initialization) or not torch.cuda.is_available()
             dev = None if cpu_init else torch.cuda.current_device()

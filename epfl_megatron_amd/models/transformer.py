@@ -30,7 +30,7 @@ from ..parallel.buffers import divide, make_viewless_tensor
 from ..parallel import tensor as tp
 from ..ops.dropout import bias_dropout_add
 from ..utils.trace import trace_range, tracing
-from ..ops.norms import RMSNorm, MixedFusedLayerNorm
+from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync
 from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
 from ..ops._ext import use_native
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
@@ -91,7 +91,29 @@ class ParallelMLP(MegatronModule):
             args.ffn_hidden_size, args.hidden_size, bias=args.use_bias, input_is_parallel=True,
             init_method=output_layer_init_method, skip_bias_add=True, **_linear_kwargs(args))
 
+    def _fused_ok(self, x):
+        fc1, fc2 = self.dense_h_to_4h, self.dense_4h_to_h
+        if not self.glu_activation or self.use_bias:
+            return False
+        if not torch.is_grad_enabled() and x.numel() // x.shape[-1] <= 16:
+            return False  # decode rows: the weight-streaming skinny GEMM
+        return tp.fused_glu_mlp_supported(x, fc1.weight, fc2.weight, self.glu_activation)
+
     def forward(self, hidden_states):
+        if self._fused_ok(hidden_states):
+            # fc1 + GLU + fc2 on the NT GEMM with the GLU in its epilogues
+            fc1, fc2 = self.dense_h_to_4h, self.dense_4h_to_h
+            _param_sync(fc1.weight, fc2.weight)  # module pre-hooks are bypassed
+            x = hidden_states
+            if not (fc1.async_tensor_model_parallel_allreduce or fc1.sequence_parallel_enabled):
+                x = tp.copy_to_tensor_model_parallel_region(x)
+            out = tp.glu_mlp(x, fc1.weight, fc2.weight, self.glu_activation,
+                             sequence_parallel=fc1.sequence_parallel_enabled,
+                             tp_async_allreduce=fc1.async_tensor_model_parallel_allreduce,
+                             gradient_accumulation_fusion=fc1.gradient_accumulation_fusion)
+            if not fc2.sequence_parallel_enabled:  # (SP: reduce-scattered inside)
+                out = tp.reduce_from_tensor_model_parallel_region(out)
+            return out, None
         inter, bias = self.dense_h_to_4h(hidden_states)
         if self.glu_activation:
             if bias is not None:

@@ -38,6 +38,7 @@ _TIMING = [False]
 _STATS = OrderedDict()  # key -> [count, bytes, ms]
 _GROUP_NAMES = {}
 _PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
+_LOOPBACK = {}  # id(group) -> simulated size (--simulated_tensor_parallel_size)
 
 
 class CommRaceError(RuntimeError):
@@ -51,6 +52,22 @@ def set_race_check(enabled):
 
 def set_timing(enabled):
     _TIMING[0] = bool(enabled)
+
+
+def set_loopback(group, world):
+    """Make ``group`` (a real 1-rank group) stand for ``world`` ranks: its
+    collectives run as local copies with a real rank's traffic accounted —
+    all-gather replicates the input ``world`` times, reduce-scatter writes the
+    mean of the ``world`` chunks, all-reduce / broadcast are identities.  Used
+    by the one-GPU per-rank proxies of the TP configurations."""
+    if world and world > 1:
+        _LOOPBACK[id(group)] = int(world)
+    else:
+        _LOOPBACK.pop(id(group), None)
+
+
+def loopback_size(group):
+    return _LOOPBACK.get(id(group))
 
 
 def name_group(group, name):
@@ -183,6 +200,8 @@ def _op(op):
 def all_reduce(tensor, group=None, async_op=False, op="sum"):
     """In-place all-reduce; ``op='avg'`` averages inside the collective (ncclAvg)."""
     rop = _op(op)
+    if id(group) in _LOOPBACK:
+        return _issue("all_reduce", group, tensor, tensor, lambda a: None, async_op)
     return _issue("all_reduce", group, tensor, tensor,
                   lambda a: dist.all_reduce(tensor, op=rop, group=group, async_op=a), async_op)
 
@@ -192,6 +211,11 @@ def reduce_scatter_into(output, inp, group=None, async_op=False, op="sum"):
     ``output`` may alias the matching chunk of ``inp`` (in-place form)."""
     rop = _op(op)
     src = inp if inp.is_contiguous() else inp.contiguous()
+    n = _LOOPBACK.get(id(group))
+    if n:
+        def loop(a):
+            torch.mean(src.view(n, *output.shape), dim=0, out=output)
+        return _issue("reduce_scatter", group, src, src, loop, async_op)
     return _issue("reduce_scatter", group, src, src,
                   lambda a: dist.reduce_scatter_tensor(output, src, op=rop, group=group,
                                                        async_op=a), async_op)
@@ -201,12 +225,19 @@ def all_gather_into(output, inp, group=None, async_op=False):
     """``output`` = concat over ranks of ``inp`` along dim 0.  ``inp`` may alias
     this rank's chunk of ``output`` (in-place form)."""
     src = inp if inp.is_contiguous() else inp.contiguous()
+    n = _LOOPBACK.get(id(group))
+    if n:
+        def loop(a):
+            output.view(n, *src.shape).copy_(src.unsqueeze(0).expand(n, *src.shape))
+        return _issue("all_gather", group, output, src, loop, async_op)
     return _issue("all_gather", group, output, src,
                   lambda a: dist.all_gather_into_tensor(output, src, group=group, async_op=a),
                   async_op)
 
 
 def broadcast(tensor, src, group=None, async_op=False):
+    if id(group) in _LOOPBACK:
+        return _issue("broadcast", group, tensor, tensor, lambda a: None, async_op)
     return _issue("broadcast", group, tensor, tensor,
                   lambda a: dist.broadcast(tensor, src=src, group=group, async_op=a), async_op)
 

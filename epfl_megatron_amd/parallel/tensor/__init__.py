@@ -4,7 +4,8 @@ from .layers import (ColumnParallelLinear, RowParallelLinear, VocabParallelEmbed
                      param_is_not_tensor_parallel_duplicate,
                      set_tensor_model_parallel_attributes,
                      set_defaults_if_not_set_tensor_model_parallel_attributes,
-                     copy_tensor_model_parallel_attributes)
+                     copy_tensor_model_parallel_attributes,
+                     fused_glu_mlp_supported, glu_mlp)
 from .mappings import (copy_to_tensor_model_parallel_region,
                        gather_from_tensor_model_parallel_region,
                        gather_from_sequence_parallel_region,

@@ -35,6 +35,7 @@ from torch.nn.parameter import Parameter
 from .. import state, comm
 from ..buffers import divide, get_global_memory_buffer
 from .mappings import (copy_to_tensor_model_parallel_region,
+                       gather_along_first_dim,
                        gather_from_tensor_model_parallel_region,
                        reduce_from_tensor_model_parallel_region,
                        reduce_scatter_to_sequence_parallel_region,
@@ -257,7 +258,210 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
                  out=main_grad)
 
 
+# ---- GEMM primitives ---------------------------------------------------------
+# Forward / dgrad products and the fused GLU forms, with the row-group remaps
+# of the SP overlap.  On the GPU they run on the hand-written NT GEMM
+# (csrc/gemm_nt.hip); elsewhere (CPU / gloo tests, unsupported shapes) the
+# same contract is computed with torch ops, so the chunked-overlap and fused-
+# MLP control flow is exercised by the CPU equivalence tests too.
+_GLU_KIND = {"swiglu": 0, "geglu": 1, "reglu": 2, "liglu": 3}
+
+
+def _rows_view(t, rmap, m):
+    """Logical rows [0, m) of ``t`` under a (rows, stride, offset) map, as a view."""
+    if not rmap:
+        return t[:m]
+    R, S, O = rmap
+    return t.view(-1, S, t.shape[-1])[:, O:O + R]
+
+
+def _kernel_ok(a, w):
+    return a.is_cuda and ext().gemm_nt_supported(a, w)
+
+
+def gemm(a, w, out=None, a_map=None, c_map=None, m=None):
+    """out[c_map(q)] = a[a_map(q)] @ w^T for logical rows q < m (default: all
+    rows of ``a``).  Maps: (rows, stride, offset) — see csrc/kernels.h RowMap."""
+    m = m if m is not None else a.shape[0]
+    if _kernel_ok(a, w) and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0)):
+        return ext().gemm_nt(a, w, out, list(a_map or []), list(c_map or []), m)
+    src = _rows_view(a, a_map, m).reshape(m, a.shape[-1])
+    res = src @ w.t()
+    if out is None:
+        return res
+    _rows_view(out, c_map, m).copy_(res.view(_rows_view(out, c_map, m).shape))
+    return out
+
+
+def _act(kind, x):
+    return (F.silu(x), F.gelu(x), F.relu(x), x)[kind]
+
+
+def gemm_glu(a, w1, kind, pre=None, y=None, c_map=None):
+    """(pre, y) = (a @ w1^T, x1 * act(x2)) with x1 / x2 the up / gate halves."""
+    if _kernel_ok(a, w1):
+        return ext().gemm_nt_glu(a, w1, kind, pre, y, list(c_map or []))
+    p = a @ w1.t()
+    f = w1.shape[0] // 2
+    yy = p[:, :f] * _act(kind, p[:, f:])
+    if pre is None:
+        return p, yy
+    _rows_view(pre, c_map, a.shape[0]).copy_(p.view(_rows_view(pre, c_map, a.shape[0]).shape))
+    _rows_view(y, c_map, a.shape[0]).copy_(yy.view(_rows_view(y, c_map, a.shape[0]).shape))
+    return pre, y
+
+
+def gemm_dglu(g, w2t, pre, kind):
+    """d(pre) = GLU backward of dAct = g @ w2t^T at the saved pre-activation."""
+    if _kernel_ok(g, w2t):
+        return ext().gemm_nt_dglu(g, w2t, pre, kind)
+    da = g @ w2t.t()
+    f = w2t.shape[0]
+    x1, x2 = pre[:, :f], pre[:, f:]
+    with torch.enable_grad():
+        xg = x2.detach().requires_grad_()
+        a = _act(kind, xg)
+        (dact,) = torch.autograd.grad(a, xg, da * x1)
+    return torch.cat([da * _act(kind, x2), dact], dim=-1)
+
+
+# ---- sequence-parallel forward overlap --------------------------------------
+# Under SP a column-parallel linear all-gathers its input and a row-parallel
+# linear reduce-scatters its output.  Both are split into EMA_SP_CHUNKS pieces
+# of the local token rows: the all-gather of piece j+1 (resp. the reduce-
+# scatter of piece j) runs on RCCL's stream while the GEMM of piece j (resp.
+# j+1) runs on the compute stream; ordering is by the work handles' events.
+# A gathered piece is rank-major ([tp][R] rows); the GEMM's row-group remap
+# places it in natural [s, b] order (and reads the rows of one reduce-scatter
+# piece out of the natural order), so no permutation copy exists.  Reference:
+# megatron/core/tensor_parallel/layers.py:225-243, mappings.py:107-124 (the
+# blocking forms).
+_SP_CHUNKS = int(os.environ.get("EMA_SP_CHUNKS", "2"))
+
+
+def _sp_pieces(rows_local):
+    c = max(1, _SP_CHUNKS)
+    return c if rows_local % c == 0 else 1
+
+
+def _tp():
+    world = state.get_tensor_model_parallel_world_size()
+    return world, (state.get_tensor_model_parallel_group() if world > 1 else None)
+
+
+def sp_allgather_gemm(x_local, w, glu_kind=None):
+    """Column-parallel forward under SP: AG(x_local) @ w^T (or the fused GLU
+    pair) with the all-gather pipelined against the GEMM.  x_local [rl, K]."""
+    world, group = _tp()
+    rl, K = x_local.shape
+    c = _sp_pieces(rl)
+    R = rl // c
+    dt, dev = x_local.dtype, x_local.device
+    n = w.shape[0] if glu_kind is None else w.shape[0] // 2
+    if glu_kind is None:
+        out = torch.empty(world * rl, n, dtype=dt, device=dev)
+    else:
+        pre = torch.empty(world * rl, 2 * n, dtype=dt, device=dev)
+        y = torch.empty(world * rl, n, dtype=dt, device=dev)
+    g = get_global_memory_buffer().get_tensor((c, world * R, K), dt, "mpu")
+    works = [comm.all_gather_into(g[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
+             for j in range(c)]
+    for j in range(c):
+        works[j].wait()
+        cmap = (R, c * R, j * R) if c > 1 else None
+        if glu_kind is None:
+            gemm(g[j], w, out, c_map=cmap)
+        else:
+            gemm_glu(g[j], w, glu_kind, pre, y, c_map=cmap)
+    return out if glu_kind is None else (pre, y)
+
+
+def sp_gemm_reducescatter(x_full, w):
+    """Row-parallel forward under SP: RS(x_full @ w^T), each piece's reduce-
+    scatter overlapping the next piece's GEMM.  x_full [tp * rl, K]."""
+    world, group = _tp()
+    M = x_full.shape[0]
+    rl = M // world
+    c = _sp_pieces(rl)
+    R = rl // c
+    n = w.shape[0]
+    out = torch.empty(rl, n, dtype=x_full.dtype, device=x_full.device)
+    part = torch.empty(c, world * R, n, dtype=x_full.dtype, device=x_full.device)
+    works = []
+    for j in range(c):
+        gemm(x_full, w, part[j], a_map=(R, c * R, j * R) if c > 1 else None, m=world * R)
+        works.append(comm.reduce_scatter_into(out[j * R:(j + 1) * R], part[j], group=group,
+                                              async_op=True))
+    for wk in works:
+        wk.wait()
+    return out
+
+
+def _dgrad(g2, weight):
+    """dX = dY W: the NT kernel on the per-step cached W^T when it applies."""
+    if g2.is_cuda and _TUNED_GEMM:
+        return tuned_gemm.linear_dgrad(g2, weight)
+    wt = _weight_t(weight) if g2.is_cuda else None
+    if wt is None:
+        return g2.matmul(weight)
+    return gemm(g2, wt) if _NT_GEMM else g2.matmul(wt.t())
+
+
+def _fwd(x2, weight):
+    if x2.is_cuda and _TUNED_GEMM:
+        return tuned_gemm.linear_fwd(x2, weight)
+    return gemm(x2, weight) if (_NT_GEMM and x2.is_cuda) else x2.matmul(weight.t())
+
+
+# Plain forward / dgrad GEMMs on the hand-written NT GEMM (csrc/gemm_nt.hip)
+# instead of hipBLASLt: off by default — isolated, the NT kernel reaches 0.81-
+# 0.90x of hipBLASLt on the 7B shapes, and the 7B step measured 28.8k tok/s
+# with it vs 30.6k without (profiles/r3a_gemm_nt_bench.txt).  The fused GLU
+# forms (0.98x / 1.03x of hipBLASLt + the glu kernels) stay on.
+_NT_GEMM = os.environ.get("EMA_NT_GEMM", "0") == "1"
+
+
+def _linear_backward(input_, weight, grad_output, use_bias, gaf, async_ar, sp):
+    """Backward of Y = X W^T (+ b) for one TP rank.  ``sp``: ``input_`` is the
+    local SP shard (re-gathered here, overlapped with the dgrad GEMM) and dX is
+    reduce-scattered (overlapped with the wgrad GEMM); ``async_ar``: dX is
+    TP-all-reduced, overlapped with the wgrad GEMM."""
+    world, group = _tp()
+    tp_group = group if world > 1 else None
+    gather_handle = None
+    if sp:
+        shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
+        total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
+        gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
+    else:
+        total = input_
+    go2 = grad_output.reshape(-1, grad_output.shape[-1])
+    if not go2.is_contiguous():
+        go2 = go2.contiguous()
+    grad_input = _dgrad(go2, weight).view(*grad_output.shape[:-1], weight.shape[1])
+    if gather_handle is not None:
+        gather_handle.wait()
+    ti2 = total.reshape(-1, total.shape[-1])
+    handle = None
+    if async_ar and tp_group is not None:
+        handle = comm.all_reduce(grad_input, group=tp_group, async_op=True)
+    if sp:
+        if async_ar:
+            raise AssertionError("sequence parallel and async all-reduce are exclusive")
+        sub = torch.empty_like(input_)
+        handle = comm.reduce_scatter_into(sub, grad_input, group=tp_group, async_op=True)
+        grad_input = sub
+    grad_weight = _wgrad(weight, go2, ti2, gaf)
+    grad_bias = go2.sum(dim=0) if use_bias else None
+    if handle is not None:
+        handle.wait()
+    return grad_input, grad_weight, grad_bias
+
+
 class _LinearFn(torch.autograd.Function):
+    """Y = X W^T (+ b) of a column-parallel (or plain) linear; under SP the
+    input all-gather is pipelined against the GEMM (``sp_allgather_gemm``)."""
+
     @staticmethod
     def forward(ctx, input_, weight, bias, gradient_accumulation_fusion,
                 async_grad_allreduce, sequence_parallel):
@@ -266,18 +470,18 @@ class _LinearFn(torch.autograd.Function):
         ctx.gradient_accumulation_fusion = gradient_accumulation_fusion
         ctx.async_grad_allreduce = async_grad_allreduce
         ctx.sequence_parallel = sequence_parallel
+        K = input_.shape[-1]
+        x2 = input_.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
         if sequence_parallel:
             world = state.get_tensor_model_parallel_world_size()
-            shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
-            total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
-            comm.all_gather_into(total, input_, group=state.get_tensor_model_parallel_group())
+            out = sp_allgather_gemm(x2, weight)
+            lead = (input_.shape[0] * world,) + tuple(input_.shape[1:-1])
         else:
-            total = input_
-        if total.is_cuda and _TUNED_GEMM:
-            x2 = total.reshape(-1, total.shape[-1])
-            out = tuned_gemm.linear_fwd(x2, weight).view(*total.shape[:-1], weight.shape[0])
-        else:
-            out = torch.matmul(total, weight.t())
+            out = _fwd(x2, weight)
+            lead = tuple(input_.shape[:-1])
+        out = out.view(*lead, weight.shape[0])
         if bias is not None:
             out = out + bias
         return out
@@ -285,53 +489,155 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         input_, weight = ctx.saved_tensors
-        tp_group = state.get_tensor_model_parallel_group() \
-            if state.get_tensor_model_parallel_world_size() > 1 else None
+        gi, gw, gb = _linear_backward(input_, weight, grad_output, ctx.use_bias,
+                                      ctx.gradient_accumulation_fusion,
+                                      ctx.async_grad_allreduce, ctx.sequence_parallel)
+        return gi, gw, gb, None, None, None
+
+
+class _RowParallelSPFn(torch.autograd.Function):
+    """Row-parallel linear + sequence-parallel reduce-scatter in one function:
+    the reduce-scatter of each output piece overlaps the next piece's GEMM
+    (``sp_gemm_reducescatter``).  Backward: all-gather dY, then dgrad / wgrad."""
+
+    @staticmethod
+    def forward(ctx, input_, weight, gradient_accumulation_fusion):
+        ctx.save_for_backward(input_, weight)
+        ctx.gaf = gradient_accumulation_fusion
+        x2 = input_.reshape(-1, input_.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        world = state.get_tensor_model_parallel_world_size()
+        out = sp_gemm_reducescatter(x2, weight)
+        return out.view(input_.shape[0] // world, *input_.shape[1:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input_, weight = ctx.saved_tensors
+        full = gather_along_first_dim(grad_output.contiguous())
+        gi, gw, _ = _linear_backward(input_, weight, full, False, ctx.gaf, False, False)
+        return gi, gw, None
+
+
+# Fused GLU MLP (column-parallel fc1 -> GLU -> row-parallel fc2) on the hand-
+# written NT GEMM (csrc/gemm_nt.hip): the GLU runs in the fc1 forward epilogue
+# and its backward in the fc2 dgrad epilogue, so neither the activation nor its
+# gradient makes an extra HBM round trip.  EMA_FUSED_MLP=0 restores the
+# unfused linear + glu kernel path.
+_FUSED_MLP = os.environ.get("EMA_FUSED_MLP", "1") != "0"
+
+
+def fused_glu_mlp_supported(x, w1, w2, glu_kind):
+    """True when ``glu_mlp`` applies (GPU: the NT kernels take every product;
+    CPU: the torch forms of the same contract)."""
+    if not (_FUSED_MLP and glu_kind in _GLU_KIND and w1.dtype == x.dtype
+            and w2.dtype == x.dtype and w1.is_contiguous() and w2.is_contiguous()):
+        return False
+    H, F2 = x.shape[-1], w1.shape[0]
+    Fh = F2 // 2
+    if not (F2 % 2 == 0 and w1.shape[1] == H and tuple(w2.shape) == (H, Fh)):
+        return False
+    if not x.is_cuda:
+        return True
+    # fc1 forward [M,H]x[2F,H]; fc2 forward [M,F]x[H,F]; fc2 dgrad [M,H]x[F,H];
+    # fc1 dgrad [M,2F]x[H,2F]: every K % 32, every N % 8, bf16 / fp16
+    return (x.dtype in (torch.bfloat16, torch.float16)
+            and H % 32 == 0 and Fh % 32 == 0 and H % 8 == 0 and Fh % 8 == 0)
+
+
+class _GluMLPFn(torch.autograd.Function):
+    """GLU(X W1^T) W2^T for one TP rank.  Without SP the result is the TP-
+    partial sum (the caller reduces it, as for ``RowParallelLinear``); with SP
+    the function includes both sequence-parallel collectives, each pipelined
+    against its GEMM, and returns the local [s/tp] rows.
+
+    Forward:  [SP: pipelined AG] gemm_glu (pre-act + y) -> gemm [SP: pipelined RS].
+    Backward: [SP: AG dOut] gemm_dglu (fc2 dgrad, d(pre-act) through the GLU
+    backward) -> fc2 wgrad -> fc1 dgrad -> [TP all-reduce or SP reduce-scatter
+    of dX, async] -> fc1 wgrad.
+    Reference: ``megatron/model/transformer.py:92-123`` (ParallelMLP),
+    ``megatron/core/tensor_parallel/layers.py:201-317`` (the linear autograd)."""
+
+    @staticmethod
+    def forward(ctx, input_, w1, w2, kind, sequence_parallel, tp_async_allreduce, gaf):
+        world = state.get_tensor_model_parallel_world_size()
+        H = input_.shape[-1]
+        x2 = input_.reshape(-1, H)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        if sequence_parallel:
+            pre, y = sp_allgather_gemm(x2, w1, glu_kind=kind)
+            out = sp_gemm_reducescatter(y, w2)
+            lead = tuple(input_.shape[:-1])
+        else:
+            pre, y = gemm_glu(x2, w1, kind)
+            out = gemm(y, w2)
+            lead = tuple(input_.shape[:-1])
+        ctx.save_for_backward(input_, w1, w2, pre, y)
+        ctx.kind, ctx.sp, ctx.tp_async, ctx.gaf = kind, sequence_parallel, tp_async_allreduce, gaf
+        ctx.world = world
+        return out.view(*lead, w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        input_, w1, w2, pre, y = ctx.saved_tensors
+        world, group = _tp()
+        tp_group = group if world > 1 else None
+        g2 = grad_out.reshape(-1, grad_out.shape[-1])
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
         gather_handle = None
-        if ctx.sequence_parallel:
-            world = state.get_tensor_model_parallel_world_size()
+        if ctx.sp:
+            g2 = gather_along_first_dim(g2)  # dOut of every rank's rows
             shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
             total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
             gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
         else:
             total = input_
-        if grad_output.is_cuda and _TUNED_GEMM:
-            g2 = grad_output.reshape(-1, grad_output.shape[-1])
-            grad_input = tuned_gemm.linear_dgrad(g2, weight).view(
-                *grad_output.shape[:-1], weight.shape[1])
-        else:
-            wt = _weight_t(weight) if grad_output.is_cuda else None
-            grad_input = grad_output.matmul(weight) if wt is None else grad_output.matmul(wt.t())
+        # fc2 dgrad with the GLU backward in the epilogue: d(pre-act) [M, 2F]
+        dpre = gemm_dglu(g2, _weight_t_always(w2), pre, ctx.kind)
+        # fc1 dgrad: dX = d(pre) W1 = d(pre) (W1^T)^T
+        dx = gemm(dpre, _weight_t_always(w1)).view(*total.shape[:-1], w1.shape[1])
+        handle, sub = None, None
+        if ctx.sp:
+            sub = torch.empty_like(input_)
+            handle = comm.reduce_scatter_into(sub, dx, group=tp_group, async_op=True)
+        elif ctx.tp_async and tp_group is not None:
+            handle = comm.all_reduce(dx, group=tp_group, async_op=True)
+        # weight gradients while the dX collective runs
+        gw2 = _wgrad(w2, g2, y, ctx.gaf)
         if gather_handle is not None:
             gather_handle.wait()
-        go2 = grad_output.reshape(-1, grad_output.shape[-1])
-        ti2 = total.reshape(-1, total.shape[-1])
-        handle = None
-        if ctx.async_grad_allreduce and tp_group is not None:
-            handle = comm.all_reduce(grad_input, group=tp_group, async_op=True)
-        sub_grad_input = None
-        if ctx.sequence_parallel:
-            if ctx.async_grad_allreduce:
-                raise AssertionError("sequence parallel and async all-reduce are exclusive")
-            world = state.get_tensor_model_parallel_world_size()
-            sub_grad_input = torch.empty((input_.shape[0],) + tuple(input_.shape[1:]),
-                                         dtype=input_.dtype, device=input_.device)
-            handle = comm.reduce_scatter_into(sub_grad_input, grad_input, group=tp_group,
-                                              async_op=True)
-        if ctx.gradient_accumulation_fusion and hasattr(weight, "main_grad"):
-            _wgrad_into_main_grad(weight, go2, ti2)
-            grad_weight = None
-            _notify_grad_ready(weight)
-        else:
-            grad_weight = go2.t().matmul(ti2)
-        grad_bias = go2.sum(dim=0) if ctx.use_bias else None
-        if ctx.sequence_parallel:
-            if handle is not None:
-                handle.wait()
-            return sub_grad_input, grad_weight, grad_bias, None, None, None
+        x2 = total.reshape(-1, total.shape[-1])
+        gw1 = _wgrad(w1, dpre, x2, ctx.gaf)
         if handle is not None:
             handle.wait()
-        return grad_input, grad_weight, grad_bias, None, None, None
+        return (sub if ctx.sp else dx), gw1, gw2, None, None, None, None
+
+
+def _weight_t_always(weight):
+    """W^T, cached per training step when possible, else built now."""
+    wt = _weight_t(weight) if weight.is_cuda else None
+    if wt is not None:
+        return wt
+    return _transpose(weight) if _tn_ok(weight) else weight.t().contiguous()
+
+
+def _wgrad(weight, g2, x2, gaf):
+    """Weight gradient of Y = X W^T: into main_grad (returns None) or as a tensor."""
+    if gaf and hasattr(weight, "main_grad"):
+        _wgrad_into_main_grad(weight, g2, x2)
+        _notify_grad_ready(weight)
+        return None
+    return g2.t().matmul(x2)
+
+
+def glu_mlp(input_, w1, w2, glu_kind, *, sequence_parallel, tp_async_allreduce,
+            gradient_accumulation_fusion):
+    """Per-rank GLU MLP through the fused kernels (see ``_GluMLPFn``).  Without
+    SP the caller reduces the returned partial output across the TP group."""
+    return _GluMLPFn.apply(input_, w1, w2, _GLU_KIND[glu_kind], sequence_parallel,
+                           tp_async_allreduce, gradient_accumulation_fusion)
 
 
 # Decode-sized inference batches (<= 16 token rows, no autograd): the weight-
@@ -504,13 +810,15 @@ class RowParallelLinear(torch.nn.Module):
             if self.sequence_parallel_enabled:
                 raise AssertionError("sequence parallelism needs a parallel input")
             input_parallel = scatter_to_tensor_model_parallel_region(input_)
-        output_parallel = _skinny_linear(input_parallel, self.weight, None, False)
-        if output_parallel is None:
-            output_parallel = _LinearFn.apply(input_parallel, self.weight, None,
-                                              self.gradient_accumulation_fusion, False, False)
         if self.sequence_parallel_enabled:
-            output_ = reduce_scatter_to_sequence_parallel_region(output_parallel)
+            # GEMM + reduce-scatter pipelined in pieces (_RowParallelSPFn)
+            output_ = _RowParallelSPFn.apply(input_parallel, self.weight,
+                                             self.gradient_accumulation_fusion)
         else:
+            output_parallel = _skinny_linear(input_parallel, self.weight, None, False)
+            if output_parallel is None:
+                output_parallel = _LinearFn.apply(input_parallel, self.weight, None,
+                                                  self.gradient_accumulation_fusion, False, False)
             output_ = reduce_from_tensor_model_parallel_region(output_parallel)
         if not self.skip_bias_add:
             output = output_ + self.bias if self.bias is not None else output_

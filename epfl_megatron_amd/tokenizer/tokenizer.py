@@ -44,7 +44,8 @@ def build_tokenizer(args):
 
 def vocab_size_with_padding(orig_vocab_size, args):
     """Round up to a multiple of make_vocab_size_divisible_by * TP."""
-    multiple = args.make_vocab_size_divisible_by * args.tensor_model_parallel_size
+    tp = getattr(args, "simulated_tensor_parallel_size", None) or args.tensor_model_parallel_size
+    multiple = args.make_vocab_size_divisible_by * tp
     after = ((orig_vocab_size + multiple - 1) // multiple) * multiple
     if args.rank == 0:
         print(f" > padded vocab (size: {orig_vocab_size}) with {after - orig_vocab_size} dummy "

@@ -134,3 +134,74 @@ def test_gemm_nt_matches_unfused_path():
     dact = dy @ w2
     dpre_u = _ext().glu_bwd(dact, pre, 0)
     assert _rel_err(dpre, dpre_u) < 1e-2
+
+
+@pytest.mark.parametrize("M,H,F,kind", [
+    (512, 256, 352, "swiglu"),     # F = 11 x 32 (W^T built by torch, not transpose16)
+    (1000, 512, 1408, "swiglu"),   # ragged M
+    (300, 256, 256, "geglu"),
+])
+def test_fused_glu_mlp_fwd_bwd_vs_fp32(M, H, F, kind):
+    """fc1 + GLU + fc2 forward and backward through parallel.tensor.glu_mlp
+    (NT GEMM, GLU in the fc1 epilogue, GLU backward in the fc2 dgrad epilogue)
+    against the fp32 torch composition."""
+    from epfl_megatron_amd.parallel.tensor import glu_mlp
+    torch.manual_seed(1)
+    x = _rand(M, H).requires_grad_()
+    w1 = _rand(2 * F, H, scale=H ** -0.5).requires_grad_()
+    w2 = _rand(H, F, scale=F ** -0.5).requires_grad_()
+    dout = _rand(M, H)
+    out = glu_mlp(x, w1, w2, kind, sequence_parallel=False, tp_async_allreduce=False,
+                  gradient_accumulation_fusion=False)
+    out.backward(dout)
+    xr, w1r, w2r = (t.detach().float().requires_grad_() for t in (x, w1, w2))
+    pre = xr @ w1r.t()
+    act = torch.nn.functional.silu if kind == "swiglu" else torch.nn.functional.gelu
+    ref = (pre[:, :F] * act(pre[:, F:])) @ w2r.t()
+    ref.backward(dout.float())
+    assert _rel_err(out, ref) < 1e-2
+    assert _rel_err(x.grad, xr.grad) < 2e-2
+    assert _rel_err(w1.grad, w1r.grad) < 2e-2
+    assert _rel_err(w2.grad, w2r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("tp,c,R,N,K", [
+    (8, 2, 1024, 1536, 4096),   # 7B TP8 s4096 mbs4 rank: chunk rows = s/(tp c) * b
+    (4, 2, 200, 264, 96),       # ragged group size, ragged N
+    (2, 3, 128, 512, 64),
+])
+def test_gemm_nt_row_maps(tp, c, R, N, K):
+    """Row-group remaps of the chunked TP overlap: A rows gathered from (and C
+    rows scattered to) groups of R rows at stride c*R, offset j*R."""
+    torch.manual_seed(2)
+    b = _rand(N, K, scale=K ** -0.5)
+    full = _rand(tp * c * R, K)
+    for j in range(c):
+        out = _ext().gemm_nt(full, b, a_map=[R, c * R, j * R], m=tp * R)
+        ref = full.view(tp, c, R, K)[:, j].reshape(tp * R, K).float() @ b.float().t()
+        assert out.shape == (tp * R, N) and _rel_err(out, ref) < 1e-2
+    g = _rand(tp * R, K)
+    dst = torch.zeros(tp * c * R, N, device=DEV, dtype=torch.bfloat16)
+    j = c - 1
+    _ext().gemm_nt(g, b, dst, c_map=[R, c * R, j * R])
+    v = dst.view(tp, c, R, N)
+    assert _rel_err(v[:, j].reshape(tp * R, N), g.float() @ b.float().t()) < 1e-2
+    assert v[:, :j].abs().sum().item() == 0
+    # fused GLU with a C remap into the full pre / y
+    F = 256
+    w1 = _rand(2 * F, K, scale=K ** -0.5)
+    pre = torch.zeros(tp * c * R, 2 * F, device=DEV, dtype=torch.bfloat16)
+    y = torch.zeros(tp * c * R, F, device=DEV, dtype=torch.bfloat16)
+    _ext().gemm_nt_glu(g, w1, 0, pre, y, [R, c * R, 0])
+    p_ref = g.float() @ w1.float().t()
+    y_ref = p_ref[:, :F] * torch.nn.functional.silu(p_ref[:, F:])
+    assert _rel_err(pre.view(tp, c, R, 2 * F)[:, 0].reshape(tp * R, -1), p_ref) < 1e-2
+    assert _rel_err(y.view(tp, c, R, F)[:, 0].reshape(tp * R, -1), y_ref) < 2e-2
+    assert y.view(tp, c, R, F)[:, 1:].abs().sum().item() == 0
+
+
+def test_gemm_nt_row_map_out_of_range_refused():
+    a = _rand(256, 64)
+    b = _rand(256, 64)
+    with pytest.raises(RuntimeError):
+        _ext().gemm_nt(a, b, a_map=[128, 256, 128], m=256)  # rows 128..383 of a 256-row a

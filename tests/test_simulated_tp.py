@@ -1,0 +1,51 @@
+"""--simulated_tensor_parallel_size: one TP rank of a TP=N model in one process
+(the 1-GPU proxies of the TP configurations)."""
+import torch
+
+from dist_utils import run_dist, init_framework, TINY_LLAMA
+
+
+def _sim_rank(rank, world, n):
+    import finetune
+    init_framework(TINY_LLAMA + ["--micro_batch_size", "2", "--num_attention_heads", "8",
+                                 "--simulated_tensor_parallel_size", str(n),
+                                 "--sequence_parallel"], finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.parallel import comm, state
+    from epfl_megatron_amd.training import (_setup_model_and_optimizer,
+                                            build_train_valid_test_data_iterators, train_step)
+    args = get_args()
+    out = {"tp": state.get_tensor_model_parallel_world_size(), "sp": args.sequence_parallel}
+    g = state.get_tensor_model_parallel_group()
+    x = torch.arange(6, dtype=torch.float32).view(3, 2)
+    full = torch.empty(3 * n, 2)
+    comm.all_gather_into(full, x, group=g)
+    out["ag"] = torch.equal(full, x.repeat(n, 1))
+    parts = torch.arange(n * 6, dtype=torch.float32).view(n * 3, 2)
+    rs = torch.empty(3, 2)
+    comm.reduce_scatter_into(rs, parts, group=g)
+    out["rs"] = torch.allclose(rs, parts.view(n, 3, 2).mean(0))
+    model, opt, sched = _setup_model_and_optimizer(finetune.model_provider,
+                                                   ModelType.encoder_or_decoder, args=args)
+    shapes = {k: tuple(p.shape) for k, p in model[0].named_parameters()}
+    out["qkv"] = next(v for k, v in shapes.items() if "query_key_value" in k)
+    out["fc1"] = next(v for k, v in shapes.items() if "dense_h_to_4h" in k)
+    it = build_train_valid_test_data_iterators(finetune.train_valid_test_datasets_provider)[0]
+    comm.report(reset=True)
+    ld, _, _, _ = train_step(finetune.forward_step, it, model, opt, sched, args)
+    out["loss"] = float(ld["lm loss"])
+    out["comm"] = {k: v[0] for k, v in comm.report().items() if k.endswith("/tp")}
+    return out
+
+
+def test_simulated_tp_rank_shapes_and_loopback():
+    out = run_dist(_sim_rank, 1, 4)[0]
+    assert out["tp"] == 4 and out["sp"]
+    assert out["ag"] and out["rs"]
+    # h 64, 8 heads of 8 -> 2 heads per rank: qkv 3 * 2 * 8 = 48 rows; ffn 128 -> 2 * 32
+    assert out["qkv"] == (48, 64) and out["fc1"] == (64, 64)
+    assert out["loss"] == out["loss"] and out["loss"] > 0
+    # SP: two all-gathers (qkv, fc1) and two reduce-scatters (dense, fc2) per layer
+    # and micro-batch in the forward at least
+    assert out["comm"].get("all_gather/tp", 0) >= 4 and out["comm"].get("reduce_scatter/tp", 0) >= 4
