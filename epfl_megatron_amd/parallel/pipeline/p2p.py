@@ -13,6 +13,7 @@ Activations ``[s(/tp), b, h]`` move between adjacent stages with batched
   each TP rank sends only its 1/TP slice and the receiver all-gathers over TP.
 * Variable sequence lengths: shapes are exchanged first (int64[3]).
 """
+import contextlib
 import operator
 from functools import reduce
 
@@ -29,6 +30,21 @@ def _device():
 
 
 _PENDING_SENDS = []  # Work handles of exchanges that only sent (not yet waited)
+_DEFER = [0]  # > 0 inside a pipeline schedule: pure sends may stay in flight
+
+
+@contextlib.contextmanager
+def deferred_sends():
+    """Scope (the pipeline schedules) in which pure sends are left in flight;
+    every one of them is completed when the scope ends.  Outside it (inference,
+    evaluation, tools) a send is completed before ``send_*`` returns, so a rank
+    can never exit with its last activation still queued."""
+    _DEFER[0] += 1
+    try:
+        yield
+    finally:
+        _DEFER[0] -= 1
+        wait_pending_sends()
 
 
 def wait_pending_sends():
@@ -52,7 +68,7 @@ def _p2p(ops):
     if not ops:
         return
     group = state.get_pipeline_model_parallel_group()
-    if all(k == "send" for k, _, _ in ops):
+    if _DEFER[0] > 0 and all(k == "send" for k, _, _ in ops):
         h = comm.p2p(ops, group=group, async_op=True)
         if h is not None:
             _PENDING_SENDS.append(h)

@@ -12,6 +12,7 @@ DP gradient reduction overlaps with backward: the DDP wrapper launches bucket
 collectives during the LAST backward of each model chunk only (gradient
 accumulation across the earlier microbatches stays local).
 """
+import functools
 import contextlib
 
 import torch
@@ -211,6 +212,17 @@ def _send_backward_recv_forward(grads, shapes, timers):
             for g, s in zip(grads, shapes)]
 
 
+def _deferred_sends(fn):
+    """Run a pipelined schedule with its pure sends left in flight between
+    exchanges (``p2p.deferred_sends``)."""
+    @functools.wraps(fn)
+    def wrapper(*a, **k):
+        with p2p.deferred_sends():
+            return fn(*a, **k)
+    return wrapper
+
+
+@_deferred_sends
 def forward_backward_pipelining_without_interleaving(forward_step_func, data_iterator, model,
                                                      optimizer, timers, forward_only,
                                                      collect_non_loss_data=False):
@@ -279,6 +291,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func, data_ite
     return store
 
 
+@_deferred_sends
 def forward_backward_pipelining_with_interleaving(forward_step_func, data_iterator, model,
                                                   optimizer, timers, forward_only,
                                                   collect_non_loss_data=False):

@@ -163,7 +163,8 @@ def _notify_grad_ready(param):
 # default; EMA_WGRAD=hipblaslt for the library): 1.11-1.40 PF isolated vs
 # 0.94-1.16 PF and 28.3k vs 26.7k tokens/s in the 7B step (profiles/r2_wgrad_ab.txt).
 _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hip").lower() == "hip"
-# One 256x256 output tile per workgroup; below one tile per CU (TP-sharded
+# One 256x256 output tile per workgroup (ragged last tiles masked, so the TP=8
+# FFN shards 2752 / 1376 stay on it); below one tile per CU (TP-sharded
 # 7B/70B projections) the kernel splits the tokens over up to 8 workgroups per
 # tile (fp32 partials + ordered reduce).  Under 32 tiles hipBLASLt is used.
 _WGRAD_MIN_TILES = int(os.environ.get("EMA_WGRAD_MIN_TILES", "32"))
@@ -239,7 +240,7 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
         K = input_2d.shape[1]
         if _WGRAD_KERNEL and main_grad.is_contiguous() and grad_output_2d.is_contiguous() \
                 and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K) \
-                and (N // 256) * (K // 256) >= _WGRAD_MIN_TILES:
+                and (-(-N // 256)) * (-(-K // 256)) >= _WGRAD_MIN_TILES:
             ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
         elif _TUNED_GEMM:
             tuned_gemm.wgrad(main_grad.view(N, K), grad_output_2d, input_2d, accumulate)
@@ -283,6 +284,11 @@ def gemm(a, w, out=None, a_map=None, c_map=None, m=None):
     """out[c_map(q)] = a[a_map(q)] @ w^T for logical rows q < m (default: all
     rows of ``a``).  Maps: (rows, stride, offset) — see csrc/kernels.h RowMap."""
     m = m if m is not None else a.shape[0]
+    if not (_NT_GEMM or a_map or c_map) and a.is_cuda and m == a.shape[0]:
+        # plain product: hipBLASLt unless EMA_NT_GEMM=1 (see _NT_GEMM)
+        if out is None:
+            return a.matmul(w.t())
+        return torch.matmul(a, w.t(), out=out)
     if _kernel_ok(a, w) and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0)):
         return ext().gemm_nt(a, w, out, list(a_map or []), list(c_map or []), m)
     src = _rows_view(a, a_map, m).reshape(m, a.shape[-1])
@@ -417,7 +423,10 @@ def _fwd(x2, weight):
 # instead of hipBLASLt: off by default — isolated, the NT kernel reaches 0.81-
 # 0.90x of hipBLASLt on the 7B shapes, and the 7B step measured 28.8k tok/s
 # with it vs 30.6k without (profiles/r3a_gemm_nt_bench.txt).  The fused GLU
-# forms (0.98x / 1.03x of hipBLASLt + the glu kernels) stay on.
+# forms (0.98x / 1.03x of hipBLASLt + the glu kernels) stay on; the plain
+# products inside the fused MLP (fc2 forward, fc1 dgrad) go to hipBLASLt
+# unless a row-group remap (SP pipeline) needs the NT kernel: with them on the
+# NT kernel the step measured 30.1k vs 31.0k unfused (profiles/r3c_*).
 _NT_GEMM = os.environ.get("EMA_NT_GEMM", "0") == "1"
 
 

@@ -4,6 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+timeout -k 10 200 python -u scripts/fa_diag.py --json gpurun_out/r3c_fa_diag.json > gpurun_out/r3c_fa_diag.txt 2>&1 || { tail -20 gpurun_out/r3c_fa_diag.txt; exit 1; }
+cat gpurun_out/r3c_fa_diag.txt
 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > gpurun_out/r3c_bench_fused.log 2>&1 || { tail -20 gpurun_out/r3c_bench_fused.log; exit 1; }
 tail -1 gpurun_out/r3c_bench_fused.log
 EMA_FUSED_MLP=0 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > gpurun_out/r3c_bench_unfused.log 2>&1 || { tail -20 gpurun_out/r3c_bench_unfused.log; exit 1; }

@@ -57,8 +57,10 @@ def main():
     x, w1 = r(M, H), r(2 * F, H)
     pre, y = torch.empty(M, 2 * F, device=dev, dtype=dt), torch.empty(M, F, device=dev, dtype=dt)
     g = [x[j * tp * R:(j + 1) * tp * R] for j in range(c)]
-    cases.append(("fc1+glu", 2.0 * M * 2 * F * H, lambda: C.gemm_nt_glu(x, w1, 0, pre, y, []),
-                  lambda: [C.gemm_nt_glu(g[j], w1, 0, pre, y, [R, c * R, j * R]) for j in range(c)]))
+    cases.append(("fc1+glu", 2.0 * M * 2 * F * H,
+                  lambda x=x, w1=w1, pre=pre, y=y: C.gemm_nt_glu(x, w1, 0, pre, y, []),
+                  lambda g=g, w1=w1, pre=pre, y=y: [C.gemm_nt_glu(g[j], w1, 0, pre, y, [R, c * R, j * R])
+                                                    for j in range(c)]))
     # reduce-scatter side (attention out, fc2): the pieces read through a_map
     for name, k in (("o_proj", H // tp), ("fc2", F)):
         x, w = r(M, k), r(H, k)
