@@ -588,6 +588,123 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// Fused decode projections (csrc/skinny_gemm.hip).  x [M, K] (M <= 16),
+// w [N, K] (GLU: [2F, K]); norm_w: RMSNorm of x in the prologue; epi:
+// 0 plain, 1 residual add (res [M, N]), 2 GLU (-> [M, F]),
+// 3 QKV (-> q [M, nq * hd]; k / v written into the cache slot).
+static ema::SkinnyArgs skinny_args(const at::Tensor& x, const at::Tensor& w,
+                                   const c10::optional<at::Tensor>& norm_w, double eps) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "skinny: shapes");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "skinny: contiguous operands");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type(), "skinny: dtype mismatch");
+  const int dt = dtype_code(x);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "skinny: bf16/fp16 only");
+  check_vec_aligned(x, "x");
+  check_vec_aligned(w, "w");
+  ema::SkinnyArgs p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.M = (int)x.size(0);
+  p.K = (int)x.size(1);
+  if (norm_w) {
+    TORCH_CHECK(norm_w->is_cuda() && norm_w->is_contiguous() && norm_w->numel() == p.K &&
+                norm_w->scalar_type() == x.scalar_type(), "skinny: norm weight must be [K], x dtype");
+    p.norm_w = norm_w->data_ptr();
+    p.eps = (float)eps;
+  }
+  return p;
+}
+
+at::Tensor skinny_norm_gemm(const at::Tensor& x, const at::Tensor& w,
+                            const c10::optional<at::Tensor>& norm_w, double eps,
+                            const c10::optional<at::Tensor>& res) {
+  auto p = skinny_args(x, w, norm_w, eps);
+  const int64_t N = w.size(0);
+  TORCH_CHECK(ema::skinny_gemm_supported(p.M, N, p.K), "skinny: unsupported shape");
+  auto y = at::empty({p.M, N}, x.options());
+  p.N = (int)N;
+  p.y = y.data_ptr();
+  p.ldy = N;
+  int epi = 0;
+  if (res) {
+    TORCH_CHECK(res->is_cuda() && res->scalar_type() == x.scalar_type() && res->dim() == 2 &&
+                res->size(0) == p.M && res->size(1) == N && res->stride(1) == 1 &&
+                res->stride(0) % 8 == 0, "skinny: residual must be [M, N] rows of the x dtype");
+    check_vec_aligned(*res, "res");
+    p.res = res->data_ptr();
+    p.ldr = res->stride(0);
+    epi = 1;
+  }
+  ema::skinny_gemm_ex(p, epi, dtype_code(x), cur_stream());
+  return y;
+}
+
+at::Tensor skinny_norm_glu(const at::Tensor& x, const at::Tensor& w1,
+                           const c10::optional<at::Tensor>& norm_w, double eps, int64_t kind) {
+  auto p = skinny_args(x, w1, norm_w, eps);
+  const int64_t F = w1.size(0) / 2;
+  TORCH_CHECK(w1.size(0) == 2 * F && F % 8 == 0 &&
+              ema::skinny_gemm_supported(p.M, 2 * F, p.K), "skinny glu: unsupported shape");
+  auto y = at::empty({p.M, F}, x.options());
+  p.N = (int)F;
+  p.y = y.data_ptr();
+  p.ldy = F;
+  p.act = (int)kind;
+  ema::skinny_gemm_ex(p, 2, dtype_code(x), cur_stream());
+  return y;
+}
+
+// qkv decode projection: returns the rotated q [M, ng * r * hd]; k / v rows go
+// to kcache / vcache [L, B, ng, hd] (views at the batch offset) at the slot
+// `slot_t` (int64 device scalar) or `slot`.
+at::Tensor skinny_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w,
+                                 const c10::optional<at::Tensor>& norm_w, double eps, int64_t ng,
+                                 int64_t r, int64_t hd, const at::Tensor& cos,
+                                 const at::Tensor& sin, const at::Tensor& pos, at::Tensor kcache,
+                                 at::Tensor vcache, const c10::optional<at::Tensor>& slot_t,
+                                 int64_t slot) {
+  auto p = skinny_args(x, w, norm_w, eps);
+  const int64_t N = w.size(0);
+  TORCH_CHECK(N == ng * (r + 2) * hd && hd % 8 == 0, "skinny qkv: w rows != ng * (r + 2) * hd");
+  TORCH_CHECK(ema::skinny_gemm_supported(p.M, N, p.K), "skinny qkv: unsupported shape");
+  TORCH_CHECK(cos.is_cuda() && sin.is_cuda() && cos.scalar_type() == at::kFloat &&
+              sin.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous() &&
+              cos.size(-1) == hd / 2, "skinny qkv: rope tables fp32 [max_pos, hd/2]");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kLong && pos.size(0) == p.M,
+              "skinny qkv: pos int64 with one row per token");
+  for (const at::Tensor* c : {&kcache, &vcache}) {
+    TORCH_CHECK(c->is_cuda() && c->scalar_type() == x.scalar_type() && c->dim() == 4 &&
+                c->size(1) >= p.M && c->size(2) == ng && c->size(3) == hd && c->stride(3) == 1 &&
+                c->stride(2) == hd, "skinny qkv: caches [L, B, ng, hd] with packed heads");
+  }
+  TORCH_CHECK(kcache.stride(0) == vcache.stride(0) && kcache.stride(1) == vcache.stride(1),
+              "skinny qkv: k / v cache strides differ");
+  if (slot_t) {
+    TORCH_CHECK(slot_t->is_cuda() && slot_t->scalar_type() == at::kLong, "skinny qkv: slot int64");
+    p.slot_ptr = slot_t->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(slot >= 0 && slot < kcache.size(0), "skinny qkv: slot out of range");
+    p.slot = slot;
+  }
+  auto q = at::empty({p.M, ng * r * hd}, x.options());
+  p.N = (int)N;
+  p.y = q.data_ptr();
+  p.ldy = ng * r * hd;
+  p.r = (int)r;
+  p.hd = (int)hd;
+  p.cos = cos.data_ptr<float>();
+  p.sin = sin.data_ptr<float>();
+  p.pos = pos.data_ptr<int64_t>();
+  p.pos_sb = pos.stride(0);
+  p.kcache = kcache.data_ptr();
+  p.vcache = vcache.data_ptr();
+  p.c_ss = kcache.stride(0);
+  p.c_sb = kcache.stride(1);
+  ema::skinny_gemm_ex(p, 3, dtype_code(x), cur_stream());
+  return q;
+}
+
 // ---------------------------------------------------------------- decode attention
 // q [b, 1, nq, hd] (strides qs = (sb, ss, sg, sh)), k/v caches [b, sk, nkv, hd]
 // (strides (sb, ss, sg)), out [b, 1, nq, hd] (strides (sb, ss, sh)).
@@ -912,6 +1029,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_decode", &flash_decode);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_gemm_supported", &skinny_gemm_supported);
+  m.def("skinny_norm_gemm", &skinny_norm_gemm);
+  m.def("skinny_norm_glu", &skinny_norm_glu);
+  m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache);
   m.def("transpose16", &transpose16);
   m.def("transpose16_supported", &transpose16_supported);
 }

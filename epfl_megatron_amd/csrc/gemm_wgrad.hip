@@ -48,7 +48,9 @@
 //     CUs, or a partial last round of tiles: wgrad_plan): fp32 partials per
 //     split, then an ordered reduce into G — deterministic, unlike atomics.
 //
-// Shapes: N % 256 == 0, K % 256 == 0, M % 32 == 0 (checked by the host).
+// Shapes: N % 8 == 0, K % 8 == 0, M % 32 == 0 (checked by the host); a
+// ragged last tile row / column (e.g. the TP=8 shards of Llama-2-7B's FFN,
+// 2752 and 1376) clamps its loads and masks its stores.
 #include <cstdlib>
 
 #include "fa_common.h"
@@ -80,6 +82,8 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 template <typename T, int I0 = 0, int I1 = 2>
 __device__ __forceinline__ void stage_op(const T* __restrict__ src, int64_t ld, int64_t m0,
                                          int64_t c0, char* lds, int dst, int wave, int lane) {
+  // ld is also the column count: chunks past a ragged last tile's edge re-read
+  // the last chunk of the row (their output rows / columns are never stored)
 #pragma unroll
   for (int i = I0; i < I1; ++i) {
     const int piece = wave * 2 + i;
@@ -87,7 +91,9 @@ __device__ __forceinline__ void stage_op(const T* __restrict__ src, int64_t ld, 
     const int rem = o & 4095;
     const int row = 8 * (o >> 12) + ((rem >> 6) & 7);
     const int ch = 4 * (rem >> 9) + (((rem >> 4) & 3) ^ ((row >> 2) & 3));
-    const T* g = src + (m0 + row) * ld + c0 + ch * 8;
+    int64_t col = c0 + ch * 8;
+    col = col < ld ? col : ld - 8;
+    const T* g = src + (m0 + row) * ld + col;
     __builtin_amdgcn_global_load_lds(
         (const void*)g, (__attribute__((address_space(3))) void*)(lds + dst + piece * 1024), 16, 0,
         0);
@@ -146,7 +152,8 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   const int wn = wave >> 2, wk = wave & 3;  // wn is also the ping-pong group
 
   // tile order: XCD-contiguous, then 8 (n) x 4 (k) groups
-  const int ntn = N / TN, ntk = K / TK;
+  const int ntn = (N + TN - 1) / TN, ntk = (K + TK - 1) / TK;
+  const int Nfull = N, Kfull = K;
   // This launch covers tiles [lin0, lin0 + nlin) of the grouped tile order.
   // Split-K over tokens (ws != nullptr): workgroup b takes tile b % nlin of
   // token split b / nlin and stores its fp32 partial as a dense 256 x 256
@@ -427,18 +434,33 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       v[k] = *reinterpret_cast<const f32x4*>(reg + lr * 64 + (c ^ (16 * ((lr >> 2) & 3))));
     }
     float* gb = g + (on + wn * 128 + 64 * h + gq) * (int64_t)ldg + ok + wk * 64 + 4 * cl;
-    if (ACCUM) {
-      f32x4 o[16];
+    // ragged edge (direct stores only; split partials are dense blocks):
+    // rows n >= N and 4-float column pieces k >= K are not stored
+    const int64_t nrow0 = n0 + wn * 128 + 64 * h + gq;
+    const bool full = ws || (n0 + TN <= Nfull && k0 + TK <= Kfull);
+    const bool kok = ws || k0 + wk * 64 + 4 * cl < Kfull;
+    if (full) {
+      if (ACCUM) {
+        f32x4 o[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        o[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(gb + (int64_t)(4 * k) * ldg));
+        for (int k = 0; k < 16; ++k)
+          o[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(gb + (int64_t)(4 * k) * ldg));
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        __builtin_nontemporal_store(o[k] + v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
-    } else {
+        for (int k = 0; k < 16; ++k)
+          __builtin_nontemporal_store(o[k] + v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
+      } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
+        for (int k = 0; k < 16; ++k)
+          __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg));
+      }
+    } else if (kok) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (nrow0 + 4 * k < Nfull) {
+          f32x4* q = reinterpret_cast<f32x4*>(gb + (int64_t)(4 * k) * ldg);
+          __builtin_nontemporal_store(ACCUM ? __builtin_nontemporal_load(q) + v[k] : v[k], q);
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before reuse
   }
@@ -461,11 +483,12 @@ int tile_group(int ntn, int ntk) {
 template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
             int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1) {
-  const int ntiles = (N / TN) * (K / TK);
+  const int ntiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
   if (nlin < 0) nlin = ntiles;
   const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
   hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(nlin * nsplit), dim3(512), 0, s,
-                     (const T*)dy, (const T*)x, g, M, N, K, tile_group(N / TN, K / TK), msplit,
+                     (const T*)dy, (const T*)x, g, M, N, K,
+                     tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), msplit,
                      nsplit > 1 ? ws : nullptr, lin0, nlin);
 }
 
@@ -476,10 +499,11 @@ __global__ __launch_bounds__(256) void wgrad_split_reduce_k(const float* __restr
                                                            int gn, int lin0, int nlin, int nsplit,
                                                            int accumulate) {
   const int t = blockIdx.x / 64, part = blockIdx.x % 64;
-  const int2 tt = tile_of(lin0 + t, N / TN, K / TK, gn);
+  const int2 tt = tile_of(lin0 + t, (N + TN - 1) / TN, (K + TK - 1) / TK, gn);
   const int tn = tt.x, tk = tt.y;
   const int e = (part * 256 + threadIdx.x) * 4;  // element of the 256 x 256 block
   const int row = e / TK, col = e % TK;
+  if ((int64_t)tn * TN + row >= N || (int64_t)tk * TK + col >= K) return;  // ragged edge
   float* gp = g + ((int64_t)tn * TN + row) * K + (int64_t)tk * TK + col;
   f32x4 acc = accumulate ? *reinterpret_cast<const f32x4*>(gp) : f32x4{0.f, 0.f, 0.f, 0.f};
   for (int sp = 0; sp < nsplit; ++sp)
@@ -524,8 +548,8 @@ void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int
 }
 
 bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
-  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % TN == 0 && K % TK == 0 &&
-         M <= (int64_t)1 << 30 && (N / TN) * (K / TK) < (int64_t)1 << 31 &&
+  return M > 0 && N >= 8 && K >= 8 && M % BM == 0 && N % 8 == 0 && K % 8 == 0 &&
+         M <= (int64_t)1 << 30 && ((N + TN - 1) / TN) * ((K + TK - 1) / TK) < (int64_t)1 << 31 &&
          N * K < ((int64_t)1 << 40);
 }
 
@@ -538,7 +562,7 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
 //     tail tiles are split over the idle CUs.
 // At least 2048 tokens (64 ring subtiles) per split.
 WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K) {
-  const int tiles = (int)((N / TN) * (K / TK));
+  const int tiles = (int)(((N + TN - 1) / TN) * ((K + TK - 1) / TK));
   WgradPlan pl{tiles, tiles, 0, 1};
   auto splits_for = [&](int t) {
     int sp = (256 + t - 1) / t;
@@ -600,7 +624,8 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
     else if (dt == DT_F16)
       launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
-                       ws, g, iN, iK, tile_group(iN / TN, iK / TK), pl.tail_lin0, pl.tail_tiles,
+                       ws, g, iN, iK, tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK),
+                       pl.tail_lin0, pl.tail_tiles,
                        pl.nsplit, accumulate ? 1 : 0);
   }
 }

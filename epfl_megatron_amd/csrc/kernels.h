@@ -211,6 +211,32 @@ bool flash_attn_supported(int hd, int dt);
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K);
 void skinny_gemm(const void* x, const void* w, void* y, int64_t M, int64_t N, int64_t K, int dt,
                  hipStream_t s);
+// Fused decode forms (skinny_gemm.hip header): epi 0 plain, 1 residual add,
+// 2 GLU (N = F, W [2F, K]), 3 GQA QKV with rotary + KV-cache write.
+struct SkinnyArgs {
+  const void* x;        // [M, K]
+  const void* w;        // [N, K] (GLU: [2N, K])
+  void* y;              // [M, ldy]: output (QKV: the q heads, [M, nq * hd])
+  int M, N, K;
+  int64_t ldy;
+  const void* norm_w;   // RMSNorm weight [K] (nullptr: no norm prologue)
+  float eps;
+  const void* res;      // EPI_RES: residual [M, ldr]
+  int64_t ldr;
+  int act;              // EPI_GLU: activation kind (0 swiglu, 1 geglu, 2 reglu, 3 liglu)
+  // EPI_QKV
+  int r, hd;            // q heads per KV group, head dim (features: [ng, r + 2, hd])
+  const float* cos;     // rotary tables [max_pos, hd / 2]
+  const float* sin;
+  const int64_t* pos;   // absolute position of token m at pos[m * pos_sb]
+  int64_t pos_sb;
+  void* kcache;         // cache slot rows: cache + slot * c_ss + m * c_sb + g * hd
+  void* vcache;
+  int64_t c_ss, c_sb;
+  const int64_t* slot_ptr;  // device slot index (graph decode) or nullptr: `slot`
+  int64_t slot;
+};
+void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
 
 // ---- transpose.hip -------------------------------------------------------------------------------
 // dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.

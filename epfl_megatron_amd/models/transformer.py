@@ -19,6 +19,7 @@ are cached at KV-head count (D2), full recompute forwards ``position_ids``
 bias-GeLU fusion (D15).
 """
 import math
+import os
 from contextlib import nullcontext
 
 import torch
@@ -32,13 +33,21 @@ from ..ops.dropout import bias_dropout_add
 from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync
 from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
-from ..ops._ext import use_native
+from ..ops._ext import use_native, ext
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
 from ..ops.activations import glu, bias_gelu, gelu
 from ..ops.softmax import FusedScaleMaskSoftmax
 from .enums import AttnMaskType, AttnType, LayerType, ModelType, PositionEmbeddingType
 from .module import MegatronModule
 from .utils import attention_mask_func, erf_gelu
+
+
+# Decode steps (one new token per sequence, <= 16 sequences, TP = 1) run each
+# layer as 5 weight-streaming launches with the elementwise work fused in
+# (csrc/skinny_gemm.hip): [RMSNorm + QKV + RoPE + KV-cache write] ->
+# decode attention -> [dense + residual] -> [RMSNorm + fc1 + GLU] ->
+# [fc2 + residual].  EMA_DECODE_FUSED=0 keeps the unfused kernels.
+_DECODE_FUSED = os.environ.get("EMA_DECODE_FUSED", "1") != "0"
 
 
 def _linear_kwargs(args):
@@ -419,6 +428,72 @@ class ParallelTransformerLayer(MegatronModule):
                 and (self.hidden_dropout == 0.0 or not self.training) and self.drop_path is None
                 and hasattr(self.input_layernorm, "forward_residual"))
 
+    def _decode_fused_ok(self, hidden_states, ip):
+        """One decode step of a plain pre-RMSNorm rotary GLU block on one TP rank."""
+        if not (_DECODE_FUSED and ip is not None and not torch.is_grad_enabled()
+                and hidden_states.is_cuda and hidden_states.dim() == 3
+                and hidden_states.shape[0] == 1 and hidden_states.shape[1] <= 16
+                and hidden_states.dtype in (torch.bfloat16, torch.float16)
+                and self._fused_residual_ok()):
+            return False
+        sa, mlp = self.self_attention, self.mlp
+        if not (isinstance(self.input_layernorm, RMSNorm)
+                and isinstance(self.post_attention_layernorm, RMSNorm)
+                and sa.attention_type == AttnType.self_attn
+                and sa.position_embedding_type == PositionEmbeddingType.rotary
+                and sa.query_key_value.bias is None and sa.dense.bias is None
+                and mlp.glu_activation and not mlp.use_bias
+                and state.get_tensor_model_parallel_world_size() == 1
+                and sa.hidden_size_per_attention_head in (64, 128)):
+            return False
+        C = ext()
+        b, H = hidden_states.shape[1], hidden_states.shape[2]
+        wq, wo = sa.query_key_value.weight, sa.dense.weight
+        w1, w2 = mlp.dense_h_to_4h.weight, mlp.dense_4h_to_h.weight
+        ws = (wq, wo, w1, w2, self.input_layernorm.weight, self.post_attention_layernorm.weight)
+        if any(w.dtype != hidden_states.dtype or not w.is_contiguous() for w in ws):
+            return False
+        F2 = w1.shape[0]
+        return (F2 % 16 == 0 and C.skinny_gemm_supported(b, wq.shape[0], H)
+                and C.skinny_gemm_supported(b, H, wo.shape[1])
+                and C.skinny_gemm_supported(b, F2, H) and C.skinny_gemm_supported(b, H, F2 // 2))
+
+    def _forward_decode_fused(self, hidden_states, ip, position_ids):
+        sa, mlp = self.self_attention, self.mlp
+        ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
+        C = ext()
+        _, b, H = hidden_states.shape
+        x = hidden_states.reshape(b, H)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        if sa.layer_number not in ip.key_value_memory_dict:
+            ip.key_value_memory_dict[sa.layer_number] = sa._allocate_kv(
+                ip.max_sequence_len, ip.max_batch_size, x.device)
+        kmem, vmem = ip.key_value_memory_dict[sa.layer_number]
+        b0, s0 = ip.batch_size_offset, ip.sequence_len_offset
+        kc, vc = kmem[:, b0:b0 + b], vmem[:, b0:b0 + b]
+        cos, sin = sa._rope(x.device)
+        if position_ids is None:
+            pos = torch.full((b, 1), s0, dtype=torch.long, device=x.device)
+        else:
+            pos = position_ids[:, -1:].long()
+        graph = getattr(ip, "device_offset", None) is not None
+        ng, r, hd = sa.num_groups_per_partition, sa.q_per_group, sa.hidden_size_per_attention_head
+        q = C.skinny_qkv_rope_cache(x, sa.query_key_value.weight, ln1.weight, ln1.eps, ng, r, hd,
+                                    cos, sin, pos, kc, vc,
+                                    ip.device_offset if graph else None, 0 if graph else s0)
+        q4 = q.view(b, 1, ng * r, hd)
+        if graph:
+            o = flash_decode_cached(q4, kc.transpose(0, 1), vc.transpose(0, 1), ip.device_kv_len)
+        else:
+            o = flash_attn_func(q4, kc[:s0 + 1].transpose(0, 1), vc[:s0 + 1].transpose(0, 1),
+                                causal=True)
+        h2 = C.skinny_norm_gemm(o.reshape(b, -1), sa.dense.weight, None, 0.0, x)
+        y = C.skinny_norm_glu(h2, mlp.dense_h_to_4h.weight, ln2.weight, ln2.eps,
+                              tp.layers._GLU_KIND[mlp.glu_activation])
+        h3 = C.skinny_norm_gemm(y, mlp.dense_4h_to_h.weight, None, 0.0, h2)
+        return h3.view(1, b, H)
+
     def _forward_fused_residual(self, hidden_states, attention_mask, inference_params,
                                 position_ids):
         ln_out, residual = self.input_layernorm.forward_residual(hidden_states)
@@ -444,6 +519,8 @@ class ParallelTransformerLayer(MegatronModule):
 
     def _forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None,
                  inference_params=None, position_ids=None):
+        if self._decode_fused_ok(hidden_states, inference_params):
+            return self._forward_decode_fused(hidden_states, inference_params, position_ids)
         if self._fused_residual_ok():
             return self._forward_fused_residual(hidden_states, attention_mask, inference_params,
                                                 position_ids)

@@ -4,6 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_gpu_e2e.py -k "wgrad or skinny or decode or graph" > gpurun_out/r3d_wgrad_tests.log 2>&1 || { tail -30 gpurun_out/r3d_wgrad_tests.log; exit 1; }
+tail -2 gpurun_out/r3d_wgrad_tests.log
 for i in 1 2; do
 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > gpurun_out/r3d_bench_fused$i.log 2>&1 || { tail -20 gpurun_out/r3d_bench_fused$i.log; exit 1; }
 tail -1 gpurun_out/r3d_bench_fused$i.log | cut -c1-400

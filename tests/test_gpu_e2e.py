@@ -156,6 +156,66 @@ def test_gpu_kv_cached_decode_matches_full_forward():
     assert err < 3e-2 * max(1.0, scale), (err, scale)
 
 
+def _decode_fused_vs_unfused(rank, world):
+    """The fused decode layer (5 weight-streaming launches with norm / RoPE /
+    KV-cache write / GLU / residual inside, csrc/skinny_gemm.hip) against the
+    unfused kernels on the same prefilled cache: logits and greedy tokens."""
+    import finetune
+    init_framework(LLAMA_GQA + ["--bf16"], finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType, transformer
+    from epfl_megatron_amd.training import get_model
+    from epfl_megatron_amd.inference.forward_step import InferenceParams
+    args = get_args()
+    model = get_model(finetune.model_provider, ModelType.encoder_or_decoder, wrap_with_ddp=False)
+    _deterministic_init(model, args)
+    m = model[0].eval()
+    calls = [0]
+    orig = transformer.ParallelTransformerLayer._forward_decode_fused
+
+    def counted(self, *a, **k):
+        calls[0] += 1
+        return orig(self, *a, **k)
+    transformer.ParallelTransformerLayer._forward_decode_fused = counted
+    torch.manual_seed(6)
+    b, plen, n = 3, 21, 8
+    prompt = torch.randint(0, 512, (b, plen), device="cuda")
+    pos = torch.arange(plen + n, device="cuda")[None].expand(b, -1)
+    runs = {}
+    for fused in (True, False):
+        transformer._DECODE_FUSED = fused
+        with torch.no_grad():
+            ip = InferenceParams(b, plen + n)
+            nxt = m(prompt, pos[:, :plen], None, inference_params=ip)[:, -1].argmax(-1, keepdim=True)
+            ip.sequence_len_offset += plen
+            logits, toks = [], []
+            for t in range(plen, plen + n):
+                lg = m(nxt, pos[:, t:t + 1], None, inference_params=ip).float()
+                nxt = lg[:, -1].argmax(-1, keepdim=True)
+                logits.append(lg)
+                toks.append(nxt)
+                ip.sequence_len_offset += 1
+        runs[fused] = (torch.cat(logits, 1), torch.cat(toks, 1),
+                       [t.clone() for t in ip.key_value_memory_dict[1]])
+    transformer._DECODE_FUSED = True
+    transformer.ParallelTransformerLayer._forward_decode_fused = orig
+    lf, tf, cf = runs[True]
+    lu, tu, cu = runs[False]
+    cache_err = max(float((a[:plen + n].float() - c[:plen + n].float()).abs().max())
+                    for a, c in zip(cf, cu))
+    return (calls[0], float((lf - lu).abs().max()), float(lu.abs().max()), tf.cpu().tolist(),
+            tu.cpu().tolist(), cache_err)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_decode_matches_unfused():
+    calls, err, scale, tf, tu, cache_err = run_dist(_decode_fused_vs_unfused, 1)[0]
+    assert calls == 2 * 8, calls  # every decode step of both layers took the fused path
+    assert err < 2e-2 * max(1.0, scale), (err, scale)
+    assert tf == tu
+    assert cache_err < 5e-2, cache_err
+
+
 def _graph_decode(rank, world):
     """Greedy generation replayed from one captured hipGraph (device-side cache
     slot / key count, argmax and increments inside the graph) vs the eager

@@ -431,6 +431,84 @@ def test_skinny_gemm(M, N, K):
     assert _skinny_linear(x.view(M, 1, K), w, None, False) is None  # grad mode on: autograd path
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 1024, 512), (16, 4096, 11008), (3, 512, 384)])
+def test_skinny_fused_norm_residual(M, N, K):
+    """Decode projection with the RMSNorm prologue and the residual epilogue
+    vs the unfused kernels (rmsnorm_fwd -> skinny GEMM -> add, same roundings)."""
+    from epfl_megatron_amd.ops.norms import rms_norm
+    C = _ext()
+    torch.manual_seed(M * 7 + K)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 3
+    g = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        xn = rms_norm(x, g, 1e-5)
+        ref = (C.skinny_gemm(xn, w).float() + res.float()).to(torch.bfloat16)
+        y = C.skinny_norm_gemm(x, w, g, 1e-5, res)
+        y0 = C.skinny_norm_gemm(x, w, None, 0.0, None)
+    assert torch.equal(y0, C.skinny_gemm(x, w))
+    _close(y, ref, 2e-2, 2e-2, "norm + residual")
+    # fp32 oracle of the whole fused op
+    xf = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    _close(y, xf @ w.float().t() + res.float(), 5e-2, 2e-2, "fp32 oracle")
+
+
+@pytest.mark.parametrize("kind,name", [(0, "swiglu"), (1, "geglu")])
+@pytest.mark.parametrize("M,F,K", [(1, 11008, 4096), (8, 512, 512), (16, 1376, 4096)])
+def test_skinny_fused_glu(M, F, K, kind, name):
+    """fc1 decode projection with the norm prologue and the GLU epilogue vs
+    rmsnorm -> skinny GEMM -> glu kernel."""
+    from epfl_megatron_amd.ops.norms import rms_norm
+    from epfl_megatron_amd.ops.activations import glu
+    C = _ext()
+    torch.manual_seed(F + M)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    g = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w1 = torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) * 0.03
+    with torch.no_grad():
+        ref = glu(C.skinny_gemm(rms_norm(x, g, 1e-6), w1), name)
+        y = C.skinny_norm_glu(x, w1, g, 1e-6, kind)
+    assert y.shape == (M, F)
+    _close(y, ref, 2e-2, 2e-2, "norm + glu")
+
+
+@pytest.mark.parametrize("ng,r,hd", [(2, 2, 128), (32, 1, 128), (8, 4, 64)])
+@pytest.mark.parametrize("graph_slot", [False, True])
+def test_skinny_fused_qkv_rope_cache(ng, r, hd, graph_slot):
+    """QKV decode projection with norm + RoPE + KV-cache write vs rmsnorm ->
+    skinny GEMM -> rope_qkv_inplace -> cache copies; the cache outside the
+    written slot is untouched."""
+    from epfl_megatron_amd.ops.norms import rms_norm
+    from epfl_megatron_amd.ops.rope import rope_table, rope_qkv_inplace
+    C = _ext()
+    torch.manual_seed(ng * r + hd)
+    b, K, L, B, b0, slot = 3, 512, 40, 5, 1, 17
+    N = ng * (r + 2) * hd
+    x = torch.randn(b, K, device=DEV, dtype=torch.bfloat16)
+    g = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    cos, sin = rope_table(hd, 64, DEV)
+    pos = torch.tensor([[5], [17], [40]], device=DEV)
+    kmem = torch.randn(L, B, ng, hd, device=DEV, dtype=torch.bfloat16)
+    vmem = torch.randn(L, B, ng, hd, device=DEV, dtype=torch.bfloat16)
+    k0, v0 = kmem.clone(), vmem.clone()
+    with torch.no_grad():
+        mixed = C.skinny_gemm(rms_norm(x, g, 1e-5), w).view(1, b, ng, r + 2, hd)
+        rope_qkv_inplace(mixed, cos, sin, pos)
+        q_ref = mixed[0, :, :, :r].reshape(b, -1)
+        kc, vc = kmem[:, b0:b0 + b], vmem[:, b0:b0 + b]
+        st = torch.tensor([slot], device=DEV) if graph_slot else None
+        q = C.skinny_qkv_rope_cache(x, w, g, 1e-5, ng, r, hd, cos, sin, pos, kc, vc, st,
+                                    0 if graph_slot else slot)
+    _close(q, q_ref, 2e-2, 2e-2, "q")
+    _close(kmem[slot, b0:b0 + b], mixed[0, :, :, r], 2e-2, 2e-2, "k slot")
+    _close(vmem[slot, b0:b0 + b], mixed[0, :, :, r + 1], 2e-2, 2e-2, "v slot")
+    keep = torch.ones(L, B, dtype=torch.bool, device=DEV)
+    keep[slot, b0:b0 + b] = False
+    assert torch.equal(kmem[keep], k0[keep]) and torch.equal(vmem[keep], v0[keep])
+
+
 def test_flash_attention_kvcache_causal_offset():
     """sq < sk (decode with cache): bottom-right aligned causal mask."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
@@ -445,7 +523,9 @@ def test_flash_attention_kvcache_causal_offset():
 
 @pytest.mark.parametrize("M,N,K", [(32, 256, 256), (96, 512, 256), (1024, 768, 512),
                                    (8192, 256, 512), (16384, 1536, 512), (16544, 1280, 1024),
-                                   (16384, 4352, 4096)])
+                                   (16384, 4352, 4096),
+                                   # ragged last tiles: Llama-2-7B FFN shards at TP=8
+                                   (4096, 2752, 4096), (4096, 4096, 1376), (2048, 264, 520)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_wgrad_gemm(M, N, K, dtype):
     """Hand-written MFMA wgrad (csrc/gemm_wgrad.hip) vs fp32 reference, beta 1 and 0."""
@@ -461,7 +541,8 @@ def test_wgrad_gemm(M, N, K, dtype):
     g2 = torch.full((N, K), float("nan"), device=DEV)
     C.wgrad_gemm(dy, x, g2, False)
     _close(g2, dy.float().t() @ x.float(), atol=1e-3 * math.sqrt(M), msg="store")
-    assert not C.wgrad_supported(M, N + 128, K)
+    assert not C.wgrad_supported(M, N + 4, K)
+    assert not C.wgrad_supported(M + 16, N, K)
 
 
 def test_wgrad_plan():
@@ -473,6 +554,7 @@ def test_wgrad_plan():
     assert list(C.wgrad_plan(16384, 4352, 4096)) == [256, 256, 16, 8]
     assert list(C.wgrad_plan(16384, 1536, 512)) == [0, 0, 12, 8]
     assert list(C.wgrad_plan(1024, 768, 512)) == [6, 6, 0, 1]  # too few tokens to split
+    assert list(C.wgrad_plan(16384, 2752, 4096)) == [0, 0, 176, 2]  # ragged: 11 x 16 tiles
 
 
 def test_lt_gemm_layouts():
