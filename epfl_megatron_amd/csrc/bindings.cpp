@@ -522,16 +522,30 @@ static void set_rope(ema::AttnParams& p, const c10::optional<at::Tensor>& cos,
   }
 }
 
+// Document mask (see AttnParams): contiguous int32 [2, b, s] = (doc_start, doc_end).
+static void set_docs(ema::AttnParams& p, const c10::optional<at::Tensor>& docs) {
+  if (!(docs.has_value() && docs->defined())) return;
+  TORCH_CHECK(docs->scalar_type() == at::kInt && docs->is_contiguous() && docs->dim() == 3 &&
+              docs->size(0) == 2 && docs->size(1) == p.b && docs->size(2) == p.sq,
+              "doc bounds must be contiguous int32 [2, b, s]");
+  TORCH_CHECK(p.sq == p.sk && p.causal, "document masking needs causal self-attention (sq == sk)");
+  check_gpu(*docs, "doc bounds");
+  p.doc_start = docs->data_ptr<int>();
+  p.doc_end = p.doc_start + (int64_t)p.b * p.sq;
+}
+
 void flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
                     at::Tensor lse, int64_t b, int64_t sq, int64_t sk, int64_t nq, int64_t nkv,
                     int64_t hd, std::vector<int64_t> qs, std::vector<int64_t> ks,
                     std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale,
                     const c10::optional<at::Tensor>& rope_cos,
                     const c10::optional<at::Tensor>& rope_sin,
-                    const c10::optional<at::Tensor>& rope_pos) {
+                    const c10::optional<at::Tensor>& rope_pos,
+                    const c10::optional<at::Tensor>& docs) {
   check_gpu(q, "q");
   auto p = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
   set_rope(p, rope_cos, rope_sin, rope_pos);
+  set_docs(p, docs);
   ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
 }
 
@@ -542,10 +556,12 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
                     std::vector<int64_t> vs, std::vector<int64_t> os, bool causal, double scale,
                     const c10::optional<at::Tensor>& rope_cos,
                     const c10::optional<at::Tensor>& rope_sin,
-                    const c10::optional<at::Tensor>& rope_pos) {
+                    const c10::optional<at::Tensor>& rope_pos,
+                    const c10::optional<at::Tensor>& docs) {
   check_gpu(q, "q");
   auto f = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
   set_rope(f, rope_cos, rope_sin, rope_pos);
+  set_docs(f, docs);
   TORCH_CHECK(dout.scalar_type() == q.scalar_type(), "dout dtype mismatch");
   TORCH_CHECK(dout.stride(-1) == 1, "dout head_dim must be contiguous");
   ema::AttnBwdParams p{};

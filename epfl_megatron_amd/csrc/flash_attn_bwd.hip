@@ -19,6 +19,11 @@
 //   tiles of K/V through double-buffered LDS; recomputes S^T / dP^T with the
 //   query on the MFMA lane and accumulates dQ^T = K^T dS^T in registers.
 //
+// Document mask (optional, p.doc_start != nullptr): the dQ kernel starts each
+// query block at its first document's first key tile; the dK/dV kernel ends
+// each key block's query range at its last key's document end and masks
+// queries whose document starts after the key (doc starts streamed with LSE).
+//
 // RoPE (optional, p.rope_cos != nullptr): the forward rotated Q and K, so dQ
 // and dK come out in the rotated basis; both kernels apply R^T to them in
 // their epilogue (fp32, before the bf16 store), replacing a separate
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
   constexpr int ROWB = HD * 2;                   // bytes per Q / dO / K / V row
   constexpr int RG = 8 * ROWB;                   // bytes per 8-row group (image (a))
   constexpr int TILEB = BQ2 * ROWB;              // one Q (or dO) tile
-  constexpr int BUFB = 2 * TILEB + 2 * BQ2 * 4;  // Q, dO, lse2, -delta
+  constexpr int BUFB = 2 * TILEB + 3 * BQ2 * 4;  // Q, dO, lse2, -delta, doc start
   constexpr int PIECES = TILEB / 1024, PPW = PIECES / 4;
   constexpr int KVB = BNK * ROWB;                // K (or V) rows of one item
   constexpr int KVPW = KVB / 1024 / 4;           // 1-KiB DMA pieces per wave for K (and V)
@@ -108,7 +113,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
       qf = qf < 0 ? 0 : (qf / BQ2) * BQ2;
     }
     I.q_first = qf;
-    I.nsteps_q = p.sq > qf ? (p.sq - qf + BQ2 - 1) / BQ2 : 0;
+    int q_end = p.sq;
+    if (CAUSAL && p.doc_end) {  // no query past the last key's document sees this block
+      const int kl = I.nb * BNK + BNK - 1 < p.sk ? I.nb * BNK + BNK - 1 : p.sk - 1;
+      q_end = p.doc_end[(int64_t)I.b * p.sq + kl];
+    }
+    I.nsteps_q = q_end > qf ? (q_end - qf + BQ2 - 1) / BQ2 : 0;
     I.nsteps = r_per * I.nsteps_q;
   };
 
@@ -148,6 +158,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
       __builtin_amdgcn_global_load_lds(
           (const void*)src,
           (__attribute__((address_space(3))) void*)(base + 2 * TILEB + wave * BQ2 * 4), 4, 0, 0);
+    } else if (wave == 2 && CAUSAL && p.doc_start) {  // the rows' document starts
+      int qr = q0 + lane;
+      qr = qr < p.sq ? qr : p.sq - 1;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(p.doc_start + (int64_t)I.b * p.sq + qr),
+          (__attribute__((address_space(3))) void*)(base + 2 * TILEB + 2 * BQ2 * 4), 4, 0, 0);
     }
   };
   // K / V rows of an item into the staging image: piece byte o holds row
@@ -278,16 +294,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
           });
         });
         mfma_drain();
+        const bool docs = CAUSAL && p.doc_start;
         const bool need_mask = (q0s + 32 > p.sq) || (kbase + 32 > p.sk) ||
-                               (CAUSAL && (kbase + 31 > q0s + off));
+                               (CAUSAL && (kbase + 31 > q0s + off)) || docs;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -l24[i >> 2][i & 3]));
         if (need_mask) {
+          typedef __attribute__((ext_vector_type(4))) int i4;
+          i4 ds4[4] = {};
+          if (docs) {
+            const int* dsl = reinterpret_cast<const int*>(cst + 2 * BQ2);
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) ds4[rg] = *reinterpret_cast<const i4*>(dsl + 8 * rg);
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int qr = q0s + acc_row(i, h);
-            const bool ok = (qr < p.sq) & (key < p.sk) & (!CAUSAL | (key <= qr + off));
+            const bool ok = (qr < p.sq) & (key < p.sk) &
+                            (!CAUSAL | ((key <= qr + off) & (key >= ds4[i >> 2][i & 3])));
             sacc[i] = ok ? sacc[i] : 0.f;
           }
         }
@@ -449,6 +474,17 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     const int wt = wl > 0 ? (wl + KT - 1) / KT : 0;
     wtiles = wt < ntiles ? wt : ntiles;
   }
+  // document mask (as in the forward): start at the first row's document
+  int t0 = 0, wt0 = 0, ds_row = 0, ds_wmax = 0;
+  if (CAUSAL && p.doc_start) {
+    const int* D = p.doc_start + (int64_t)b * p.sq;
+    const int r0 = qb * BMW < p.sq ? qb * BMW : p.sq - 1;
+    const int w0 = q0w < p.sq ? q0w : p.sq - 1, w1 = q0w + 31 < p.sq ? q0w + 31 : p.sq - 1;
+    t0 = D[r0] / KT;
+    wt0 = D[w0] / KT;
+    ds_wmax = D[w1];
+    ds_row = D[qrow_c];
+  }
 
   // K / V tiles arrive by LDS-DMA (global_load_lds_dwordx4: lane-linear LDS
   // image; the image-(a) layout (ia_off) is produced through the per-lane
@@ -480,8 +516,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
           (__attribute__((address_space(3))) void*)(kl + KT * ROWB + pc * 1024), 16, 0, 0);
     }
   };
-  if (ntiles > 0) prefetch(0, 0);
-  if (NB == 3 && ntiles > 1) prefetch(1, 1);
+  if (t0 < ntiles) prefetch(t0, t0 % NB);
+  if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB);
 
   x8 qf[KS], df[KS];
 #pragma unroll
@@ -525,7 +561,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   }
   __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
 
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t0; t < ntiles; ++t) {
     const int buf = t % NB;
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
     // retired before the barrier that ended tile t-1
@@ -534,7 +570,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     const char* vl = kl + KT * ROWB;
     const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
     const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
-    if (t < wtiles) {
+    if (t < wtiles && t >= wt0) {
       static_for<KT / 32>([&](auto subc) {
         constexpr int sub = decltype(subc)::value;
         const int kb = t * KT + sub * 32;
@@ -556,7 +592,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
         }
         mfma_drain();
         const bool need_mask = (kb + 32 > p.sk) || (q0w + 32 > p.sq) ||
-                               (CAUSAL && kb + 31 > q0w + off);
+                               (CAUSAL && (kb + 31 > q0w + off || kb < ds_wmax));
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -lse2));
@@ -564,7 +600,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int kr = kb + acc_row(i, h);
-            const bool ok = (kr < p.sk) & (qrow < p.sq) & (!CAUSAL | (kr <= qrow + off));
+            const bool ok = (kr < p.sk) & (qrow < p.sq) & (!CAUSAL | ((kr <= qrow + off) & (kr >= ds_row)));
             sacc[i] = ok ? sacc[i] : 0.f;
           }
         }

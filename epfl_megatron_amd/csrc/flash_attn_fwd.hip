@@ -24,6 +24,10 @@
 // Query blocks are dispatched on a flat grid, heaviest causal blocks of ALL
 // heads first.  LSE is written in natural log.
 //
+// Document mask (p.doc_start set, packed sequences): each query block starts
+// at the key tile of its first row's document; keys before a row's document
+// start are masked like the causal upper triangle.
+//
 // Fused RoPE (p.rope_cos set): Q is rotated in registers right after its load
 // and written back in place (only this workgroup reads those rows), so the
 // backward sees rotated Q; K is rotated by a k-only pre-pass (rope.hip).
@@ -81,6 +85,18 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     const int wt = wl > 0 ? (wl + KT - 1) / KT : 0;
     wtiles = wt < ntiles ? wt : ntiles;
   }
+  // document mask: the block starts at its first row's document, each wave at
+  // its own first row's; keys below a row's document start are masked
+  int t0 = 0, wt0 = 0, ds_row = 0, ds_wmax = 0;
+  if (CAUSAL && p.doc_start) {
+    const int* D = p.doc_start + (int64_t)b * p.sq;
+    const int r0 = mb * BMW < p.sq ? mb * BMW : p.sq - 1;
+    const int w0 = m0 < p.sq ? m0 : p.sq - 1, w1 = m0 + 31 < p.sq ? m0 + 31 : p.sq - 1;
+    t0 = D[r0] / KT;
+    wt0 = D[w0] / KT;
+    ds_wmax = D[w1];
+    ds_row = D[qrow_c];
+  }
 
   int srow[PPW], schunk[PPW];
 #pragma unroll
@@ -105,8 +121,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
                                        16, 0, 0);
     }
   };
-  if (ntiles > 0) prefetch(0, 0);
-  if (NB == 3 && ntiles > 1) prefetch(1, 1);
+  if (t0 < ntiles) prefetch(t0, t0 % NB);
+  if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB);
 
   x8 qf[KS];
 #pragma unroll
@@ -139,11 +155,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   }
   __syncthreads();  // vmcnt(0) + barrier: tile 0 (and 1) landed
 
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t0; t < ntiles; ++t) {
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
     // retired before the barrier that ended tile t-1
     if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
-    if (t < wtiles) {
+    if (t < wtiles && t >= wt0) {
       const int n0 = t * KT;
       const char* kl = lds + (t % NB) * 2 * TB;
       const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
@@ -172,15 +188,15 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
           });
         });
       });
-      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off) : (n0 + KT > p.sk);
+      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax) : (n0 + KT > p.sk);
       if (need_mask) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int k0 = n0 + acc_row(i, h), k1 = k0 + 32;
           bool ok0 = k0 < p.sk, ok1 = k1 < p.sk;
           if (CAUSAL) {
-            ok0 = ok0 && (k0 <= qrow + off);
-            ok1 = ok1 && (k1 <= qrow + off);
+            ok0 = ok0 && (k0 <= qrow + off) && (k0 >= ds_row);
+            ok1 = ok1 && (k1 <= qrow + off) && (k1 >= ds_row);
           }
           if (!ok0) s0[i] = -INFINITY;
           if (!ok1) s1[i] = -INFINITY;

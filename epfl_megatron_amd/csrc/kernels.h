@@ -116,6 +116,14 @@ struct AttnParams {
   const float* rope_sin;
   const int64_t* rope_pos;  // [b, s] position ids (row stride rope_pos_sb) or null: row index
   int64_t rope_pos_sb;
+  // Optional document (varlen) mask for packed sequences (--reset_attention_mask,
+  // sq == sk): int32 [b, s] first position of the document holding each
+  // position, and [b, s] one past its last position.  Key k is visible to
+  // query q iff doc_start[q] <= k (<= q under the causal mask): the forward /
+  // dQ kernels start each query block at its first document's first key tile,
+  // the dK/dV kernel stops each key block at its last document's end.
+  const int* doc_start;
+  const int* doc_end;
 };
 struct AttnBwdParams {
   AttnParams f;

@@ -294,9 +294,13 @@ class ParallelAttention(MegatronModule):
         elif self.use_flash_attn:
             rng = tp.get_cuda_rng_tracker().fork() if not self.sequence_parallel else nullcontext()
             with rng:
+                # packed documents (--reset_attention_mask): the mask arrives as
+                # int32 [2, b, s] document bounds (utils/misc.py doc_bounds)
+                docs = attention_mask if (attention_mask is not None and
+                                          attention_mask.dtype == torch.int32) else None
                 ctx = flash_attn_qkvpacked(mixed, self.num_groups_per_partition, self.q_per_group,
                                            self.hidden_size_per_attention_head, causal=True,
-                                           rope=rope, position_ids=position_ids)
+                                           rope=rope, position_ids=position_ids, doc_bounds=docs)
         else:
             q, k, v = self._split_qkv(mixed)
             if rope is not None:

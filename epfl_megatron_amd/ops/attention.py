@@ -32,8 +32,11 @@ from .rope import rope_qkv_inplace, apply_rope_ref
 # --------------------------------------------------------------------------
 # Reference math (CPU path + test oracle)
 # --------------------------------------------------------------------------
-def attention_ref(q, k, v, causal=True, softmax_scale=None, return_lse=False):
-    """q ``[b, sq, nq, d]``, k/v ``[b, sk, nkv, d]`` -> ``[b, sq, nq, d]`` (fp32 math)."""
+def attention_ref(q, k, v, causal=True, softmax_scale=None, return_lse=False, doc_bounds=None):
+    """q ``[b, sq, nq, d]``, k/v ``[b, sk, nkv, d]`` -> ``[b, sq, nq, d]`` (fp32 math).
+
+    ``doc_bounds``: optional int32 ``[2, b, s]`` (document start, end) of
+    packed sequences: query i sees key j only if ``doc_start[i] <= j``."""
     b, sq, nq, d = q.shape
     sk, nkv = k.shape[1], k.shape[2]
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(d)
@@ -46,6 +49,10 @@ def attention_ref(q, k, v, causal=True, softmax_scale=None, return_lse=False):
         i = torch.arange(sq, device=q.device)[:, None]
         j = torch.arange(sk, device=q.device)[None, :]
         s = s.masked_fill(j > i + (sk - sq), float("-inf"))
+    if doc_bounds is not None:
+        j = torch.arange(sk, device=q.device)[None, None, :]
+        before = j < doc_bounds[0].to(q.device).long()[:, :, None]  # [b, sq, sk]
+        s = s.masked_fill(before[:, None], float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
     p = torch.softmax(s, dim=-1)
     o = torch.matmul(p, vf).permute(0, 2, 1, 3).to(q.dtype)
@@ -93,7 +100,7 @@ def _bsnd_strides(t, r):
 
 class _FlashQKVPackedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, ng, r, hd, causal, scale, cos, sin, position_ids):
+    def forward(ctx, qkv, ng, r, hd, causal, scale, cos, sin, position_ids, docs):
         s, b = qkv.shape[0], qkv.shape[1]
         qkv5 = qkv.view(s, b, ng, r + 2, hd)
         if position_ids is not None and position_ids.dtype != torch.int64:
@@ -107,14 +114,14 @@ class _FlashQKVPackedFn(torch.autograd.Function):
         os_ = (out.stride(1), out.stride(0), out.stride(2))
         ext().flash_attn_fwd(q, k, v, out, lse, b, s, s, nq, ng, hd,
                              list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale),
-                             cos, sin, position_ids)
-        ctx.save_for_backward(qkv, out, lse, cos, sin, position_ids)
+                             cos, sin, position_ids, docs)
+        ctx.save_for_backward(qkv, out, lse, cos, sin, position_ids, docs)
         ctx.meta = (ng, r, hd, causal, scale)
         return out.view(s, b, nq * hd)
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, out, lse, cos, sin, position_ids = ctx.saved_tensors
+        qkv, out, lse, cos, sin, position_ids, docs = ctx.saved_tensors
         ng, r, hd, causal, scale = ctx.meta
         s, b = qkv.shape[0], qkv.shape[1]
         nq = ng * r
@@ -128,8 +135,8 @@ class _FlashQKVPackedFn(torch.autograd.Function):
         os_ = (out.stride(1), out.stride(0), out.stride(2))
         ext().flash_attn_bwd(dout, q, k, v, out, lse, dq, dk, dv, b, s, s, nq, ng, hd,
                              list(qs), list(ks), list(ks), list(os_), bool(causal), float(scale),
-                             cos, sin, position_ids)
-        return dqkv5.view(s, b, -1), None, None, None, None, None, None, None, None
+                             cos, sin, position_ids, docs)
+        return dqkv5.view(s, b, -1), None, None, None, None, None, None, None, None, None
 
 
 def _flash_decode(q, k, v, scale, kv_len=None):
@@ -174,7 +181,7 @@ class _FlashFn(torch.autograd.Function):
         os_ = (out.stride(0), out.stride(1), out.stride(2))
         ext().flash_attn_fwd(q, k, v, out, lse, b, sq, sk, nq, nkv, d,
                              list(qs), list(ks), list(vs), list(os_), bool(causal), float(scale),
-                             None, None, None)
+                             None, None, None, None)
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.causal, ctx.scale = causal, scale
         return out
@@ -193,27 +200,34 @@ class _FlashFn(torch.autograd.Function):
         os_ = (out.stride(0), out.stride(1), out.stride(2))
         ext().flash_attn_bwd(dout, q, k, v, out, lse, dq, dk, dv, b, sq, sk, nq, nkv, d,
                              list(qs), list(ks), list(ks), list(os_), bool(ctx.causal),
-                             float(ctx.scale), None, None, None)
+                             float(ctx.scale), None, None, None, None)
         return dq, dk, dv, None, None
 
 
 def flash_attn_qkvpacked(qkv, num_groups, q_per_group, head_dim, causal=True,
-                         softmax_scale=None, rope=None, position_ids=None):
+                         softmax_scale=None, rope=None, position_ids=None, doc_bounds=None):
     """qkv ``[s, b, ng*(r+2)*hd]`` -> context ``[s, b, ng*r*hd]``.
 
-    ``rope`` = (cos, sin) tables or None."""
+    ``rope`` = (cos, sin) tables or None.  ``doc_bounds``: int32 ``[2, b, s]``
+    document (start, end) per position for packed sequences
+    (``--reset_attention_mask``; :func:`utils.misc.doc_bounds`), or None."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(head_dim)
     cos, sin = rope if rope is not None else (None, None)
+    if doc_bounds is not None:
+        if not causal:
+            raise ValueError("document masking is defined for causal attention only")
+        doc_bounds = doc_bounds.to(device=qkv.device, dtype=torch.int32).contiguous()
     if use_native(qkv):
         return _FlashQKVPackedFn.apply(qkv, num_groups, q_per_group, head_dim, causal, scale,
-                                       cos, sin, position_ids)
+                                       cos, sin, position_ids, doc_bounds)
     s, b = qkv.shape[0], qkv.shape[1]
     qkv5 = qkv.view(s, b, num_groups, q_per_group + 2, head_dim)
     q, k, v = _split_qkv5(qkv5)
     if cos is not None:
         q = apply_rope_ref(q, cos, sin, position_ids)
         k = apply_rope_ref(k, cos, sin, position_ids)
-    o = attention_ref(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1), causal, scale)
+    o = attention_ref(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1), causal, scale,
+                      doc_bounds=doc_bounds)
     return o.transpose(0, 1).reshape(s, b, -1)
 
 

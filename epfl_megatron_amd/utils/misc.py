@@ -64,34 +64,50 @@ def report_memory(name):
         print(f"[Rank {dist.get_rank() if dist.is_initialized() else 0}] {s}", flush=True)
 
 
+def doc_bounds(data, eod_token):
+    """Document bounds of packed sequences: int32 ``[2, b, s]`` with, per
+    position, the first position of its document and one past its last.
+    A document ends WITH its EOD token (the EOD row still sees its own
+    document; the row after it starts a new one), as in the reference's
+    mask loop (``megatron/utils.py:137-194``)."""
+    b, s = data.shape
+    pos = torch.arange(s, device=data.device)
+    is_eod = data == eod_token
+    starts = torch.zeros((b, s), dtype=torch.long, device=data.device)
+    starts[:, 1:] = torch.where(is_eod[:, :-1], pos[1:], 0)
+    start = torch.cummax(starts, dim=1).values
+    ends = torch.where(is_eod, pos + 1, s)
+    end = torch.flip(torch.cummin(torch.flip(ends, [1]), dim=1).values, [1])
+    return torch.stack([start, end]).to(torch.int32).contiguous()
+
+
 def get_ltor_masks_and_position_ids(data, eod_token, reset_position_ids, reset_attention_mask,
-                                    eod_mask_loss):
+                                    eod_mask_loss, flash_doc_bounds=False):
     """Causal mask (True = masked) ``[1 or b, 1, s, s]``, loss mask and position ids.
 
     With reset flags, positions / attention restart after every EOD token of
-    each sample (reference ``megatron/utils.py:137-194``)."""
+    each sample (reference ``megatron/utils.py:137-194``), computed from
+    :func:`doc_bounds` without a per-EOD loop.  ``flash_doc_bounds``: with
+    ``reset_attention_mask``, return the int32 ``[2, b, s]`` document bounds
+    in place of the dense mask (the flash-attention kernels mask documents
+    from them; no ``b x s x s`` tensor is built)."""
     b, s = data.size()
-    att_b = b if reset_attention_mask else 1
-    attention_mask = torch.tril(torch.ones((att_b, s, s), device=data.device)).view(att_b, 1, s, s)
     loss_mask = torch.ones(data.size(), dtype=torch.float, device=data.device)
     if eod_mask_loss:
         loss_mask[data == eod_token] = 0.0
     position_ids = torch.arange(s, dtype=torch.long, device=data.device)
     position_ids = position_ids.unsqueeze(0).expand_as(data)
+    bounds = doc_bounds(data, eod_token) if (reset_position_ids or reset_attention_mask) else None
     if reset_position_ids:
-        position_ids = position_ids.clone()
-    if reset_position_ids or reset_attention_mask:
-        for i in range(b):
-            eod_idx = (data[i] == eod_token).nonzero(as_tuple=False).view(-1).tolist()
-            prev = 0
-            for j in eod_idx:
-                if reset_attention_mask:
-                    attention_mask[i, 0, (j + 1):, :(j + 1)] = 0
-                if reset_position_ids:
-                    position_ids[i, (j + 1):] -= (j + 1 - prev)
-                    prev = j + 1
-    attention_mask = attention_mask < 0.5
-    return attention_mask, loss_mask, position_ids
+        position_ids = (position_ids - bounds[0].long()).contiguous()
+    if reset_attention_mask and flash_doc_bounds:
+        return bounds, loss_mask, position_ids
+    i = torch.arange(s, device=data.device)[:, None]
+    j = torch.arange(s, device=data.device)[None, :]
+    masked = (j > i)[None]  # [1, s, s]
+    if reset_attention_mask:
+        masked = masked | (j[None] < bounds[0].long()[:, :, None])  # [b, s, s]
+    return masked.unsqueeze(1), loss_mask, position_ids
 
 
 def _rank():

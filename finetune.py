@@ -52,7 +52,7 @@ def get_batch(data_iterator):
     tokens = tokens_[:, :-1].contiguous()
     attention_mask, loss_mask, position_ids = get_ltor_masks_and_position_ids(
         tokens, tokenizer.eod, args.reset_position_ids, args.reset_attention_mask,
-        args.eod_mask_loss)
+        args.eod_mask_loss, flash_doc_bounds=args.use_flash_attn)
     return tokens, labels, loss_mask, attention_mask, position_ids
 
 

@@ -43,7 +43,7 @@ def main():
         for causal in (True, False):
             def run():
                 C.flash_attn_fwd(q, k, v, out, lse, b, s, s, nq, nq, hd, qs, ks, ks, os_, causal,
-                                 hd ** -0.5, None, None, None)
+                                 hd ** -0.5, None, None, None, None)
             run()
             torch.cuda.synchronize()
             ts = []

@@ -25,6 +25,6 @@ ks = [k.stride(0), k.stride(1), k.stride(2)]
 for _ in range(5):
     C.flash_attn_fwd(q, k, v, out, lse, b, s, s, nq, nkv, hd, qs, ks, ks,
                      [out.stride(0), out.stride(1), out.stride(2)], bool(causal), hd ** -0.5,
-                     None, None, None)
+                     None, None, None, None)
 torch.cuda.synchronize()
 print("done", flush=True)

@@ -393,6 +393,63 @@ def test_flash_attention_qkvpacked_rope(s, b, ng, r, hd, with_pos):
     _close(x.grad.cpu(), xr.grad, 6e-2, 6e-2, "qkvpacked bwd")
 
 
+def _packed_tokens(b, s, seed, eod=0):
+    """Token rows of packed documents: EODs at random places, including
+    adjacent EODs (1-token documents), one near the start and a long tail."""
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randint(1, 100, (b, s), generator=g)
+    for i in range(b):
+        n = int(torch.randint(1, 9, (1,), generator=g))
+        pos = torch.randint(0, s, (n,), generator=g)
+        t[i, pos] = eod
+        if i == 0 and s > 70:
+            t[i, 2] = eod
+            t[i, 63:65] = eod  # 1-token document straddling a 64-key tile edge
+    return t
+
+
+@pytest.mark.parametrize("s,b,ng,r,hd", [
+    (600, 2, 2, 3, 128),    # GQA, 4-wave grid, dK/dV split over query heads
+    (1024, 4, 32, 1, 128),  # Llama-2-7B heads at seq 1k: 8-wave grid, dK/dV kernel epilogue
+    (333, 3, 1, 8, 64),     # MQA, head_dim 64
+])
+def test_flash_attention_document_mask(s, b, ng, r, hd):
+    """Packed-document (varlen) masking in the flash kernels (--reset_attention_mask):
+    fwd and bwd of the training path against the fp32 reference with the
+    same document mask, fused RoPE on and position ids reset per document."""
+    from epfl_megatron_amd.ops.attention import flash_attn_qkvpacked
+    from epfl_megatron_amd.ops.rope import rope_table
+    from epfl_megatron_amd.utils.misc import get_ltor_masks_and_position_ids
+    tokens = _packed_tokens(b, s, seed=s + b).to(DEV)
+    docs, _, pos = get_ltor_masks_and_position_ids(tokens, 0, True, True, False,
+                                                    flash_doc_bounds=True)
+    assert docs.dtype == torch.int32 and docs.shape == (2, b, s)
+    cos, sin = rope_table(hd, 8192, DEV)
+    torch.manual_seed(s)
+    x = torch.randn(s, b, ng * (r + 2) * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_qkvpacked(x.clone(), ng, r, hd, causal=True, rope=(cos, sin), position_ids=pos,
+                             doc_bounds=docs)
+    ref_dev = DEV if s * s * b * ng * r > 2 ** 26 else "cpu"  # big cases: fp32 reference on the GPU
+    xr = x.detach().float().to(ref_dev).requires_grad_()
+    orf = flash_attn_qkvpacked(xr, ng, r, hd, causal=True,
+                               rope=(cos.to(ref_dev), sin.to(ref_dev)),
+                               position_ids=pos.to(ref_dev), doc_bounds=docs.to(ref_dev),
+                               ) if ref_dev == "cpu" else None
+    if orf is None:  # GPU fp32 reference: the math path on cuda tensors
+        from epfl_megatron_amd.ops.attention import attention_ref, _split_qkv5
+        from epfl_megatron_amd.ops.rope import apply_rope_ref
+        q, k, v = _split_qkv5(xr.view(s, b, ng, r + 2, hd))
+        q = apply_rope_ref(q, cos, sin, pos)
+        k = apply_rope_ref(k, cos, sin, pos)
+        orf = attention_ref(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1), True,
+                            hd ** -0.5, doc_bounds=docs).transpose(0, 1).reshape(s, b, -1)
+    _close(o.float().cpu(), orf.detach().float().cpu(), 3e-2, 3e-2, "doc-masked fwd")
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float().to(ref_dev))
+    _close(x.grad.float().cpu(), xr.grad.float().cpu(), 6e-2, 6e-2, "doc-masked bwd")
+
+
 @pytest.mark.parametrize("b,sk,nq,nkv,hd", [(2, 1, 8, 8, 128), (2, 77, 8, 2, 128),
                                               (1, 300, 71, 1, 64), (3, 1000, 64, 8, 128),
                                               (1, 4096, 32, 32, 128), (2, 513, 12, 4, 64)])
