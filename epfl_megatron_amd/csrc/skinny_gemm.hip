@@ -10,8 +10,10 @@
 // many loads in flight:
 //   * workgroup = 8 waves (4 when K % 256 != 0) = 16 output features (rows of
 //     W); wave w reduces the K slice [w K/8, (w+1) K/8) with v_mfma_f32_16x16x32 (A = 16 W rows x
-//     32 k, B = the <= 16 X rows x 32 k; unused B columns are zero), 8 k-steps
-//     of W loads issued ahead of their MFMAs;
+//     32 k, B = the <= 16 X rows x 32 k; unused B columns are zero) from a
+//     register ring that keeps SKINNY_U k-steps of W / X loads in flight
+//     (each slot refilled as soon as its MFMA has consumed it, the first
+//     block issued at kernel entry, before the RMSNorm prologue);
 //   * the per-wave partial 16 x 16 tiles are added through LDS and wave 0 writes
 //     the M x 16 block of Y (fixed order: deterministic).
 // Grid = N / 16 workgroups (256 .. 2000 on the 7B shapes).
@@ -32,6 +34,7 @@
 //     the step is graph-capturable).
 // Shapes: M <= 16, N % 16 == 0, K % 128 == 0 (checked by the host).
 #include <cstdlib>
+#include <type_traits>
 
 #include "act_math.h"
 #include "common.h"
@@ -58,89 +61,11 @@ __device__ __forceinline__ int64_t w_row(int blk, int r, int N) {
   else return (int64_t)blk * 16 + r;
 }
 
-template <typename T, int WAVES, bool NORM, int EPI, int ACT>
-__global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) {
-  typedef typename fa::MT<T>::x8 x8;
-  constexpr int U = 8;  // k-steps of loads in flight per wave
-  __shared__ f4 part[WAVES][64];
-  __shared__ float ssq[WAVES][16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int M = p.M, N = p.N, K = p.K;
-  const T* __restrict__ x = (const T*)p.x;
-  const T* __restrict__ w = (const T*)p.w;
-  const int kq = K / WAVES, kbeg = wave * kq;
-  const int r = lane & 15, kc = 8 * (lane >> 4);  // fragment row / k offset of this lane
-  const T* wr = w + w_row<EPI>(blockIdx.x, r, N) * K + kbeg + kc;
-  const bool xon = r < M;
-  const T* xr = x + (int64_t)(xon ? r : 0) * K + kbeg + kc;
-  const int steps = kq / 32;
-
-  float rs = 1.f;  // rstd of X row r (NORM)
-  const T* gr = nullptr;
-  if constexpr (NORM) {
-    gr = (const T*)p.norm_w + kbeg + kc;
-    float ss = 0.f;
-    for (int s = 0; s < steps; ++s) {
-      const x8 v = *reinterpret_cast<const x8*>(xr + 32 * s);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)v[e];
-        ss += f * f;
-      }
-    }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 16) ssq[wave][lane] = ss;
-    __syncthreads();
-    float tot = 0.f;
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
-    rs = rsqrtf(tot / (float)K + p.eps);
-  }
-  // B operand: X (or its RMSNorm, rounded like rmsnorm_fwd_k) for k-step s
-  auto bop = [&](const x8& v, int s) {
-    if constexpr (!NORM) {
-      return v;
-    } else {
-      const x8 g = *reinterpret_cast<const x8*>(gr + 32 * s);
-      x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const T xn = (T)((float)v[e] * rs);
-        o[e] = (T)((float)xn * (float)g[e]);
-      }
-      return o;
-    }
-  };
-
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  int s = 0;
-  for (; s + U <= steps; s += U) {
-    x8 a[U], bv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * (s + u)));
-      bv[u] = *reinterpret_cast<const x8*>(xr + 32 * (s + u));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      x8 b = bop(bv[u], s + u);
-      if (!xon) b = x8{};
-      acc = mfma16x16x32<T>(a[u], b, acc);
-    }
-  }
-  for (; s < steps; ++s) {
-    const x8 a = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * s));
-    x8 b = bop(*reinterpret_cast<const x8*>(xr + 32 * s), s);
-    if (!xon) b = x8{};
-    acc = mfma16x16x32<T>(a, b, acc);
-  }
-  part[wave][lane] = acc;
-  __syncthreads();
-  if (wave != 0) return;
-  f4 t = part[0][lane];
-#pragma unroll
-  for (int i = 1; i < WAVES; ++i) t += part[i][lane];  // fixed order: deterministic
+// Output of one 16-feature block (t = the block's reduced fp32 tile; lane
+// holds column m = lane & 15, features 4 (lane >> 4) + i).
+template <typename T, int EPI, int ACT>
+__device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4& t, int lane) {
+  const int M = p.M;
   // D layout: lane holds column m = lane & 15, rows (features) 4 (lane >> 4) + i
   const int m = lane & 15, nr = 4 * (lane >> 4);
   typename fa::MT<T>::x4 o;
@@ -156,12 +81,12 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
       typename fa::MT<T>::x4 out;
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[i] = (T)((float)o[i] * act<ACT>((float)gt[i]));
-      *reinterpret_cast<typename fa::MT<T>::x4*>(y + (int64_t)m * p.ldy + blockIdx.x * 8 + nr) = out;
+      *reinterpret_cast<typename fa::MT<T>::x4*>(y + (int64_t)m * p.ldy + blk * 8 + nr) = out;
     }
     return;
   }
   if (m >= M) return;
-  const int n = blockIdx.x * 16 + nr;
+  const int n = blk * 16 + nr;
   if constexpr (EPI == EPI_RES) {
     const typename fa::MT<T>::x4 rv =
         *reinterpret_cast<const typename fa::MT<T>::x4*>((const T*)p.res + (int64_t)m * p.ldr + n);
@@ -196,33 +121,313 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
   *reinterpret_cast<typename fa::MT<T>::x4*>(y + (int64_t)m * p.ldy + n) = o;
 }
 
+#ifndef SKINNY_U
+#define SKINNY_U 8  // k-steps of W / X (/ gamma) loads in flight per wave
+#endif
+
 template <typename T, int WAVES, bool NORM, int EPI, int ACT>
-void launch(const SkinnyArgs& p, hipStream_t s) {
-  const dim3 grid((unsigned)(EPI == EPI_GLU ? p.N / 8 : p.N / 16));
-  hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT>), grid, dim3(64 * WAVES), 0, s, p);
+__global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) {
+  typedef typename fa::MT<T>::x8 x8;
+  constexpr int U = SKINNY_U;
+  __shared__ f4 part[WAVES][64];
+  __shared__ float ssq[WAVES][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int M = p.M, N = p.N, K = p.K;
+  const T* __restrict__ x = (const T*)p.x;
+  const T* __restrict__ w = (const T*)p.w;
+  const int kq = K / WAVES, kbeg = wave * kq;
+  const int r = lane & 15, kc = 8 * (lane >> 4);  // fragment row / k offset of this lane
+  const T* wr = w + w_row<EPI>(blockIdx.x, r, N) * K + kbeg + kc;
+  const bool xon = r < M;
+  const T* xr = x + (int64_t)(xon ? r : 0) * K + kbeg + kc;
+  const T* gr = NORM ? (const T*)p.norm_w + kbeg + kc : nullptr;
+  const int steps = kq / 32;
+  const int nblk = steps / U;  // full ring blocks; the < U leftover steps run after them
+
+  // Ring of U k-steps: the W fragment (nontemporal: each weight byte is read
+  // once per step), the X fragment and (NORM) the gamma fragment, refilled
+  // U steps ahead right after each MFMA consumes its slot, so U k-steps of
+  // loads stay in flight through the whole stream.  Issued BEFORE the RMSNorm
+  // prologue: the weight stream starts at kernel entry, not after the norm's
+  // reduction and barrier.
+  x8 a[U], xv[U], gv[U];
+  if (nblk > 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
+      xv[u] = *reinterpret_cast<const x8*>(xr + 32 * u);
+      if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * u);
+    }
+  }
+
+  float rs = 1.f;  // rstd of X row r (NORM)
+  if constexpr (NORM) {
+    // sum of squares of this wave's X slice: 8 loads issued per round before
+    // any is used (a load-then-use loop waits out one L2 round trip per step)
+    float ss = 0.f;
+    for (int s0 = 0; s0 < steps; s0 += 8) {
+      x8 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int s = s0 + i < steps ? s0 + i : steps - 1;
+        v[i] = *reinterpret_cast<const x8*>(xr + 32 * s);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float keep = s0 + i < steps ? 1.f : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)v[i][e];
+          ss += keep * f * f;
+        }
+      }
+    }
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 16) ssq[wave][lane] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
+    rs = rsqrtf(tot / (float)K + p.eps);
+  }
+  // B operand: X (or its RMSNorm, rounded like rmsnorm_fwd_k)
+  auto bop = [&](const x8& v, const x8& g) {
+    x8 o;
+    if constexpr (!NORM) {
+      o = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const T xn = (T)((float)v[e] * rs);
+        o[e] = (T)((float)xn * (float)g[e]);
+      }
+    }
+    if (!xon) o = x8{};
+    return o;
+  };
+
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  // one ring block; REFILL: reload each slot U steps ahead once consumed
+  auto block = [&](int blk, auto refill_c) {
+    constexpr bool REFILL = decltype(refill_c)::value;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc = mfma16x16x32<T>(a[u], bop(xv[u], gv[u]), acc);
+      if constexpr (REFILL) {
+        const int s = (blk + 1) * U + u;
+        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * s));
+        xv[u] = *reinterpret_cast<const x8*>(xr + 32 * s);
+        if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * s);
+      }
+      // keep {MFMA u, refill u} in program order: hipcc would otherwise
+      // cluster the dependent MFMA chain and issue every refill after it,
+      // draining the ring (vmcnt(0)) once per block
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int blk = 0; blk + 1 < nblk; ++blk) block(blk, std::true_type{});
+  if (nblk > 0) block(nblk - 1, std::false_type{});
+  // leftover steps (K / WAVES not a multiple of 32 U): loads first, then MFMAs
+  {
+    const int s0 = nblk * U, left = steps - s0;
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u) {
+      if (u < left) {
+        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * (s0 + u)));
+        xv[u] = *reinterpret_cast<const x8*>(xr + 32 * (s0 + u));
+        if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + u));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (u < left) acc = mfma16x16x32<T>(a[u], bop(xv[u], gv[u]), acc);
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  f4 t = part[0][lane];
+#pragma unroll
+  for (int i = 1; i < WAVES; ++i) t += part[i][lane];  // fixed order: deterministic
+  epilogue<T, EPI, ACT>(p, blockIdx.x, t, lane);
 }
 
-template <typename T, int WAVES>
+// Persistent form for K = 8 waves x 32 x STEPS (STEPS 16 / 32: the 4096 / 8192
+// hidden sizes of Llama-2-7B / 70B), one workgroup per CU walking the output
+// blocks blockIdx.x, +grid, ...:
+//   * the wave's X slice (RMSNorm applied for NORM) is loaded ONCE into
+//     registers (STEPS fragments; rows >= M stay zero and are never loaded)
+//     and reused by every block: no per-block X / gamma traffic and one norm
+//     prologue per workgroup instead of one per 16 output features (the
+//     non-persistent NORM forms spent ~half their time in that prologue:
+//     profiles/r3g_decode_b8_kernels.txt);
+//   * the W ring runs across block seams: the last U refills of a block load
+//     the next block's first U k-steps, so the stream never drains;
+//   * per block, the 8 partial tiles meet in a double-buffered LDS slot and
+//     wave 0 runs the epilogue while the other waves stream the next block.
+#ifndef SKINNY_PU
+#define SKINNY_PU 8
+#endif
+template <typename T, bool NORM, int EPI, int ACT, int STEPS>
+__global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
+  typedef typename fa::MT<T>::x8 x8;
+  constexpr int WAVES = 8, U = SKINNY_PU;
+  static_assert(STEPS % U == 0, "ring must tile the k-steps");
+  __shared__ f4 part[2][WAVES][64];
+  __shared__ float ssq[WAVES][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int M = p.M, N = p.N, K = p.K;
+  const T* __restrict__ x = (const T*)p.x;
+  const T* __restrict__ w = (const T*)p.w;
+  const int kbeg = wave * STEPS * 32;
+  const int r = lane & 15, kc = 8 * (lane >> 4);
+  const bool xon = r < M;
+  const int nblocks = EPI == EPI_GLU ? N / 8 : N / 16;
+  const int G = (int)gridDim.x;
+  auto wptr = [&](int blk) { return w + w_row<EPI>(blk, r, N) * K + kbeg + kc; };
+  int blk = blockIdx.x;
+  const T* wr = wptr(blk);
+  const T* wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
+
+  x8 a[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
+  x8 xs[STEPS];
+  {
+    const T* xr = x + (int64_t)r * K + kbeg + kc;
+    if (xon) {
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) xs[s] = *reinterpret_cast<const x8*>(xr + 32 * s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) xs[s] = x8{};
+    }
+  }
+  if constexpr (NORM) {
+    const T* gr = (const T*)p.norm_w + kbeg + kc;
+    float ss = 0.f;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)xs[s][e];
+        ss += f * f;
+      }
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 16) ssq[wave][lane] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
+    const float rs = rsqrtf(tot / (float)K + p.eps);
+    // rounded like rmsnorm_fwd_k; gamma in chunks of 8 fragments (all STEPS
+    // at once would hold 2 x STEPS fragments live and spill at STEPS = 32)
+#pragma unroll
+    for (int s0 = 0; s0 < STEPS; s0 += 8) {
+      x8 g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + i));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const T xn = (T)((float)xs[s0 + i][e] * rs);
+          xs[s0 + i][e] = (T)((float)xn * (float)g[i][e]);
+        }
+        if (!xon) xs[s0 + i] = x8{};
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // one block's k-steps; LAST: the workgroup's final block, whose last U
+  // slots are not refilled (a one-block workgroup would otherwise fetch U of
+  // its STEPS k-steps twice)
+  auto run_block = [&](auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      acc = mfma16x16x32<T>(a[s % U], xs[s], acc);
+      if (!LAST || s + U < STEPS) {
+        const T* src = s + U < STEPS ? wr + 32 * (s + U) : wn + 32 * (s + U - STEPS);
+        a[s % U] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(src));
+      }
+      __builtin_amdgcn_sched_barrier(0);  // {MFMA s, refill s} in program order
+    }
+    return acc;
+  };
+  for (int j = 0;; ++j) {
+    const bool last = blk + G >= nblocks;
+    const f4 acc = last ? run_block(std::true_type{}) : run_block(std::false_type{});
+    part[j & 1][wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      f4 t = part[j & 1][0][lane];
+#pragma unroll
+      for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][lane];  // fixed order
+      epilogue<T, EPI, ACT>(p, blk, t, lane);
+    }
+    if (last) break;
+    blk += G;
+    wr = wn;
+    wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
+  }
+}
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, c = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 256;
+    return c;
+  }();
+  return n;
+}
+
+// STEPS = 0: one workgroup per output block (skinny_gemm_k); 16 / 32: the
+// persistent skinny_pgemm_k on min(blocks, CUs) workgroups.
+template <typename T, int WAVES, int STEPS, bool NORM, int EPI, int ACT>
+void launch(const SkinnyArgs& p, hipStream_t s) {
+  const int nblocks = EPI == EPI_GLU ? p.N / 8 : p.N / 16;
+  if constexpr (STEPS == 0) {
+    hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT>), dim3((unsigned)nblocks),
+                       dim3(64 * WAVES), 0, s, p);
+  } else {
+    const int g = nblocks < num_cus() ? nblocks : num_cus();
+    hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS>), dim3((unsigned)g), dim3(512), 0,
+                       s, p);
+  }
+}
+
+template <typename T, int WAVES, int STEPS>
 void dispatch(const SkinnyArgs& p, int epi, hipStream_t s) {
   const bool nm = p.norm_w != nullptr;
+  // the bf16 RMSNorm prologue over 32 register-resident k-steps spills: the
+  // normed 8192-wide forms keep the one-block-per-workgroup kernel
+  constexpr int SN = STEPS == 32 ? 0 : STEPS;
+#define EMA_SK(NORM_, EPI_, ACT_) launch<T, WAVES, (NORM_ ? SN : STEPS), NORM_, EPI_, ACT_>(p, s)
   switch (epi) {
     case EPI_RES:
-      nm ? launch<T, WAVES, true, EPI_RES, 0>(p, s) : launch<T, WAVES, false, EPI_RES, 0>(p, s);
+      nm ? EMA_SK(true, EPI_RES, 0) : EMA_SK(false, EPI_RES, 0);
       break;
     case EPI_QKV:
-      nm ? launch<T, WAVES, true, EPI_QKV, 0>(p, s) : launch<T, WAVES, false, EPI_QKV, 0>(p, s);
+      nm ? EMA_SK(true, EPI_QKV, 0) : EMA_SK(false, EPI_QKV, 0);
       break;
     case EPI_GLU:
       switch (p.act) {
-        case 0: nm ? launch<T, WAVES, true, EPI_GLU, 0>(p, s) : launch<T, WAVES, false, EPI_GLU, 0>(p, s); break;
-        case 1: nm ? launch<T, WAVES, true, EPI_GLU, 1>(p, s) : launch<T, WAVES, false, EPI_GLU, 1>(p, s); break;
-        case 2: nm ? launch<T, WAVES, true, EPI_GLU, 2>(p, s) : launch<T, WAVES, false, EPI_GLU, 2>(p, s); break;
-        default: nm ? launch<T, WAVES, true, EPI_GLU, 3>(p, s) : launch<T, WAVES, false, EPI_GLU, 3>(p, s); break;
+        case 0: nm ? EMA_SK(true, EPI_GLU, 0) : EMA_SK(false, EPI_GLU, 0); break;
+        case 1: nm ? EMA_SK(true, EPI_GLU, 1) : EMA_SK(false, EPI_GLU, 1); break;
+        case 2: nm ? EMA_SK(true, EPI_GLU, 2) : EMA_SK(false, EPI_GLU, 2); break;
+        default: nm ? EMA_SK(true, EPI_GLU, 3) : EMA_SK(false, EPI_GLU, 3); break;
       }
       break;
     default:
-      nm ? launch<T, WAVES, true, EPI_PLAIN, 0>(p, s) : launch<T, WAVES, false, EPI_PLAIN, 0>(p, s);
+      nm ? EMA_SK(true, EPI_PLAIN, 0) : EMA_SK(false, EPI_PLAIN, 0);
   }
+#undef EMA_SK
 }
 
 }  // namespace
@@ -235,14 +440,26 @@ bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
 // 8 waves (K split 8 ways) where K allows: twice the loads in flight per CU
 // of the 4-wave form, which left the N = 4096 projections (one workgroup per
 // CU) latency-bound at ~3.2 TB/s.  EMA_SKINNY_WAVES=4 forces the 4-wave form.
+// K = 4096 / 8192 (16 / 32 k-steps per wave) take the persistent form
+// (EMA_SKINNY_PERSIST=0: the one-block-per-workgroup kernel everywhere).
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s) {
   static const int want = [] {
     const char* e = getenv("EMA_SKINNY_WAVES");
     return e ? atoi(e) : 8;
   }();
+  static const bool persist = [] {
+    const char* e = getenv("EMA_SKINNY_PERSIST");
+    return !(e && e[0] == '0');
+  }();
   const bool w8 = want == 8 && p.K % 256 == 0;
-  if (dt == DT_BF16) w8 ? dispatch<bf16, 8>(p, epi, s) : dispatch<bf16, 4>(p, epi, s);
-  else w8 ? dispatch<fp16, 8>(p, epi, s) : dispatch<fp16, 4>(p, epi, s);
+  const int steps = w8 ? p.K / 256 : 0;
+  if (persist && w8 && (steps == 16 || steps == 32)) {
+    if (dt == DT_BF16) steps == 16 ? dispatch<bf16, 8, 16>(p, epi, s) : dispatch<bf16, 8, 32>(p, epi, s);
+    else steps == 16 ? dispatch<fp16, 8, 16>(p, epi, s) : dispatch<fp16, 8, 32>(p, epi, s);
+    return;
+  }
+  if (dt == DT_BF16) w8 ? dispatch<bf16, 8, 0>(p, epi, s) : dispatch<bf16, 4, 0>(p, epi, s);
+  else w8 ? dispatch<fp16, 8, 0>(p, epi, s) : dispatch<fp16, 4, 0>(p, epi, s);
 }
 
 void skinny_gemm(const void* x, const void* w, void* y, int64_t M, int64_t N, int64_t K, int dt,

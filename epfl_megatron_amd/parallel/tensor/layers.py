@@ -665,7 +665,10 @@ def _skinny_linear(input_, weight, bias, sequence_parallel):
     n = weight.shape[0]
     if m > 16 or not weight.is_contiguous() or not ext().skinny_gemm_supported(m, n, k):
         return None
-    if (m > 8 and n > 16384) or (m > 4 and n > 24576):  # hipBLASLt's wide tiles win there
+    # K = 4096 / 8192 run the persistent skinny kernel, faster than hipBLASLt up
+    # to the LM head at 16 rows; the per-block form loses to hipBLASLt's wide
+    # tiles on wide outputs (profiles/r3i_skinny_persistent_ab.txt)
+    if k not in (4096, 8192) and ((m > 8 and n > 16384) or (m > 4 and n > 24576)):
         return None
     x2 = input_.reshape(m, k)
     if not x2.is_contiguous():
