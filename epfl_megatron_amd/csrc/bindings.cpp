@@ -450,6 +450,18 @@ void opt_prep(const at::Tensor& norm_sq, const c10::optional<at::Tensor>& inv_sc
 }
 
 // ---------------------------------------------------------------- attention
+// Diagnostics: a uint64 buffer of 8 stamps per attention workgroup, attached
+// to every following launch until cleared (scripts/fa_stamps.py).
+static unsigned long long* g_fa_stamps = nullptr;
+void fa_set_stamps(const c10::optional<at::Tensor>& buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "stamps: int64 buffer");
+    g_fa_stamps = reinterpret_cast<unsigned long long*>(buf->data_ptr<int64_t>());
+  } else {
+    g_fa_stamps = nullptr;
+  }
+}
+
 ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                           const at::Tensor& out, const at::Tensor& lse, int64_t b, int64_t sq,
                           int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
@@ -494,6 +506,7 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   p.o_sb = os[0]; p.o_ss = os[1]; p.o_sh = os[2];
   p.causal = causal ? 1 : 0;
   p.scale = (float)scale;
+  p.stamps = g_fa_stamps;
   return p;
 }
 
@@ -1042,6 +1055,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_bwd", &bias_dropout_add_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("fa_set_stamps", &fa_set_stamps);
   m.def("flash_decode", &flash_decode);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_gemm_supported", &skinny_gemm_supported);

@@ -154,6 +154,14 @@ __device__ __forceinline__ typename MT<T>::x8 acc_frag(const f32x16& acc, int s)
   return r;
 }
 
+// Diagnostics (AttnParams::stamps): 10-ns wall clock, CU and XCD of the wave.
+__device__ __forceinline__ unsigned long long wall_stamp() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xf;
+}
+
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
 // ---- fused RoPE (Meta-Llama interleaved pairs (x[2j], x[2j+1]), fp32) ------
@@ -179,12 +187,9 @@ __device__ __forceinline__ void rope_inv4(float (&x)[4], const float* c, const f
     x[2 * i + 1] = x1 * cc[i] - x0 * sn[i];
   }
 }
-// R on an 8-element 16-bit fragment starting at head-dim index 2*j0 (j0 % 4 == 0).
+// R on an 8-element 16-bit fragment with the 4 (cos, sin) pairs given.
 template <typename T>
-__device__ __forceinline__ typename MT<T>::x8 rope_fwd8(typename MT<T>::x8 v, const float* c,
-                                                        const float* s, int j0) {
-  const rf4 cc = *reinterpret_cast<const rf4*>(c + j0);
-  const rf4 sn = *reinterpret_cast<const rf4*>(s + j0);
+__device__ __forceinline__ typename MT<T>::x8 rope_fwd8v(typename MT<T>::x8 v, rf4 cc, rf4 sn) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float x0 = (float)v[2 * i], x1 = (float)v[2 * i + 1];
@@ -192,6 +197,31 @@ __device__ __forceinline__ typename MT<T>::x8 rope_fwd8(typename MT<T>::x8 v, co
     v[2 * i + 1] = (T)(x0 * sn[i] + x1 * cc[i]);
   }
   return v;
+}
+// R on an 8-element 16-bit fragment starting at head-dim index 2*j0 (j0 % 4 == 0).
+template <typename T>
+__device__ __forceinline__ typename MT<T>::x8 rope_fwd8(typename MT<T>::x8 v, const float* c,
+                                                        const float* s, int j0) {
+  return rope_fwd8v<T>(v, *reinterpret_cast<const rf4*>(c + j0), *reinterpret_cast<const rf4*>(s + j0));
+}
+// R on the KS fragments of one query row (fragment kk at head-dim 16 kk + 8 h):
+// every table load issued before any is used (a load-use pair per fragment
+// would wait out KS L2 round trips), half of the fragments at a time.
+template <typename T, int KS>
+__device__ __forceinline__ void rope_rows_fwd(typename MT<T>::x8 (&qf)[KS], const float* c,
+                                              const float* s, int h) {
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    rf4 cc[KS / 2], sn[KS / 2];
+#pragma unroll
+    for (int i = 0; i < KS / 2; ++i) {
+      const int j0 = (half * (KS / 2) + i) * 8 + 4 * h;
+      cc[i] = *reinterpret_cast<const rf4*>(c + j0);
+      sn[i] = *reinterpret_cast<const rf4*>(s + j0);
+    }
+#pragma unroll
+    for (int i = 0; i < KS / 2; ++i) qf[half * (KS / 2) + i] = rope_fwd8v<T>(qf[half * (KS / 2) + i], cc[i], sn[i]);
+  }
 }
 
 // 16-byte-chunk XOR swizzle for [rows][HD] tiles that are read both by rows

@@ -54,6 +54,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   __shared__ __attribute__((aligned(1024))) char lds[NB * 2 * TB];
 
   const int tid = threadIdx.x;
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  if (p.stamps) st0 = fa::wall_stamp();
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nmb = (p.sq + BMW - 1) / BMW;
@@ -130,11 +132,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   if (p.rope_cos) {
     const float *rc, *rs;
     rope_rows<HD>(p, b, qrow_c, rc, rs);
-    T* Qw = const_cast<T*>(Q) + (int64_t)qrow * p.q_ss + 8 * h;
+    rope_rows_fwd<T, KS>(qf, rc, rs, h);  // table loads batched (not one round trip per fragment)
+    if (qrow < p.sq) {
+      T* Qw = const_cast<T*>(Q) + (int64_t)qrow * p.q_ss + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      qf[kk] = rope_fwd8<T>(qf[kk], rc, rs, kk * 8 + 4 * h);
-      if (qrow < p.sq) *reinterpret_cast<x8*>(Qw + kk * 16) = qf[kk];
+      for (int kk = 0; kk < KS; ++kk) *reinterpret_cast<x8*>(Qw + kk * 16) = qf[kk];
     }
   }
 
@@ -154,6 +156,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
              8 * (tp & 1);
   }
   __syncthreads();  // vmcnt(0) + barrier: tile 0 (and 1) landed
+  if (p.stamps) st1 = fa::wall_stamp();
 
   for (int t = t0; t < ntiles; ++t) {
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
@@ -248,6 +251,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     }
   }
 
+  if (p.stamps) st2 = fa::wall_stamp();
   if (qrow < p.sq) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
     T* O = (T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow * p.o_ss + (int64_t)head * p.o_sh;
@@ -264,6 +268,15 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     if (h == 0) {
       const float lse = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
       p.lse[((int64_t)b * p.nq + head) * p.sq + qrow] = lse;
+    }
+  }
+  if (p.stamps) {  // diagnostics (scripts/fa_stamps.py)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores done
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long* so = p.stamps + (int64_t)lin * 8;
+      so[0] = st0; so[1] = st1; so[2] = st2; so[3] = fa::wall_stamp();
+      so[4] = __smid(); so[5] = fa::xcc_id();
     }
   }
 }

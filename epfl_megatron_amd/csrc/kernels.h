@@ -124,6 +124,9 @@ struct AttnParams {
   // the dK/dV kernel stops each key block at its last document's end.
   const int* doc_start;
   const int* doc_end;
+  // Diagnostics only (null in production): per-workgroup s_memrealtime
+  // stamps [entry, prologue done, loop done, exit, cu, xcc, 0, 0] (fa_set_stamps).
+  unsigned long long* stamps;
 };
 struct AttnBwdParams {
   AttnParams f;
