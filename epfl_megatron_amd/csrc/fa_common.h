@@ -176,16 +176,34 @@ __device__ __forceinline__ void rope_rows(const AttnParams& p, int b, int row, c
   c = p.rope_cos + pos * (HD / 2);
   s = p.rope_sin + pos * (HD / 2);
 }
-// R^T on 4 consecutive fp32 elements starting at head-dim index 2*j0 (j0 even).
-__device__ __forceinline__ void rope_inv4(float (&x)[4], const float* c, const float* s, int j0) {
-  const rf2 cc = *reinterpret_cast<const rf2*>(c + j0);
-  const rf2 sn = *reinterpret_cast<const rf2*>(s + j0);
+// R^T on 4 consecutive fp32 elements with their 2 (cos, sin) pairs given.
+__device__ __forceinline__ void rope_inv4v(float (&x)[4], rf2 cc, rf2 sn) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const float x0 = x[2 * i], x1 = x[2 * i + 1];
     x[2 * i] = x0 * cc[i] + x1 * sn[i];
     x[2 * i + 1] = x1 * cc[i] - x0 * sn[i];
   }
+}
+// R^T on 4 consecutive fp32 elements starting at head-dim index 2*j0 (j0 even).
+__device__ __forceinline__ void rope_inv4(float (&x)[4], const float* c, const float* s, int j0) {
+  rope_inv4v(x, *reinterpret_cast<const rf2*>(c + j0), *reinterpret_cast<const rf2*>(s + j0));
+}
+// The (cos, sin) pairs of an accumulator-layout epilogue row (element groups
+// (d, rg) at head-dim d*32 + 8*rg + 4*h), all loaded before any is used: the
+// per-group load-then-use form waits out 2 DT 4 L2 round trips, each behind
+// the stores already issued (profiles: the dQ epilogue).
+template <int DT>
+__device__ __forceinline__ void rope_inv_tables(rf2 (&cc)[DT][4], rf2 (&sn)[DT][4], const float* c,
+                                                const float* s, int h) {
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      const int j0 = (d * 32 + 8 * rg + 4 * h) / 2;
+      cc[d][rg] = *reinterpret_cast<const rf2*>(c + j0);
+      sn[d][rg] = *reinterpret_cast<const rf2*>(s + j0);
+    }
 }
 // R on an 8-element 16-bit fragment with the 4 (cos, sin) pairs given.
 template <typename T>

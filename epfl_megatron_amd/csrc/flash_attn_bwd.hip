@@ -363,7 +363,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
         T* DK = (T*)P.dk + (int64_t)cur.b * p.k_sb + (int64_t)cur.g * p.k_sg + (int64_t)key * p.k_ss;
         T* DV = (T*)P.dv + (int64_t)cur.b * p.v_sb + (int64_t)cur.g * p.v_sg + (int64_t)key * p.v_ss;
         const float *rc = nullptr, *rs = nullptr;
-        if (p.rope_cos) rope_rows<HD>(p, cur.b, key, rc, rs);
+        rf2 rcc[DT][4], rsn[DT][4];
+        if (p.rope_cos) {
+          rope_rows<HD>(p, cur.b, key, rc, rs);
+          rope_inv_tables<DT>(rcc, rsn, rc, rs, h);
+        }
 #pragma unroll
         for (int d = 0; d < DT; ++d) {
 #pragma unroll
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
             float f[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) f[e] = dk[d][4 * rg + e] * p.scale;
-            if (rc) rope_inv4(f, rc, rs, (d * 32 + 8 * rg + 4 * h) / 2);
+            if (rc) rope_inv4v(f, rcc[d][rg], rsn[d][rg]);
             x4 wk, wv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -632,7 +636,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     T* DQ = (T*)P.dq + (int64_t)b * p.q_sb + (int64_t)qrow * p.q_ss + (int64_t)g * p.q_sg +
             (int64_t)hh * p.q_sh;
     const float *rc = nullptr, *rs = nullptr;
-    if (p.rope_cos) rope_rows<HD>(p, b, qrow, rc, rs);
+    rf2 rcc[DT][4], rsn[DT][4];
+    if (p.rope_cos) {
+      rope_rows<HD>(p, b, qrow, rc, rs);
+      rope_inv_tables<DT>(rcc, rsn, rc, rs, h);
+    }
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
 #pragma unroll
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
         float f[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) f[e] = dq[d][4 * rg + e] * p.scale;
-        if (rc) rope_inv4(f, rc, rs, (d * 32 + 8 * rg + 4 * h) / 2);
+        if (rc) rope_inv4v(f, rcc[d][rg], rsn[d][rg]);
         x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = (T)f[e];

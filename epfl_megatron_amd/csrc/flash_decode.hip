@@ -31,6 +31,8 @@
 //
 // Reference: megatron/text_generation/forward_step.py drives the per-token
 // forward; the reference decodes through the training attention path.
+#include <type_traits>
+
 #include "common.h"
 #include "fa_common.h"
 #include "kernels.h"
@@ -45,6 +47,9 @@ constexpr int DCH = 256;  // keys per chunk (= threads per workgroup)
 template <typename T, int HD, int RH>
 __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   constexpr int HP = HD / 64;  // head-dim elements per lane in P.V (1 or 2)
+  typedef typename fa::MT<T>::x8 x8;
+  // HP consecutive 16-bit values of one V row (one dword at hd 128)
+  typedef typename std::conditional<HP == 2, uint32_t, uint16_t>::type vpair;
   __shared__ float qs[RH][HD];
   __shared__ float ps[RH][DCH];
   __shared__ float red[4][RH];
@@ -59,8 +64,8 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   const int sk = p.kv_len ? min(*p.kv_len, p.sk) : p.sk;
   const int nk = min(DCH, sk - k0);
   const float sl2 = p.scale * 1.4426950408889634f;
+  const int nsplit = gridDim.x;
   if (nk <= 0) {  // chunk past the cached length (hipGraph decode): empty partial
-    const int nsplit = gridDim.x;
     for (int i = tid; i < nh * HD; i += 256) {
       const int head = g * r + h0 + i / HD;
       p.ws_o[(((int64_t)b * p.nq + head) * nsplit + chunk) * HD + i % HD] = 0.f;
@@ -73,6 +78,36 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
     return;
   }
 
+  // Every global load of the chunk is issued before anything waits: this
+  // lane's K row (scores, lane = key), the V rows of this wave's keys (P.V,
+  // lane = head-dim pair; rows past the length clamp to a valid one; all 64
+  // for MHA) and the query vectors.  The earlier form waited out a load round trip
+  // for Q, one for K and eight for V (8 rows in flight per lane), which made
+  // this ~14 us kernel the largest non-GEMM cost of a decode step
+  // (profiles/r3n_decode_b1_kernels.txt).
+  const int key = k0 + (tid < nk ? tid : nk - 1);
+  const T* krow = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)key * p.k_ss + (int64_t)g * p.k_sg;
+  // (4-8 heads per workgroup: K is read inside the score loop, where the
+  // scheduler does not hoist every query read beside 16 live K fragments)
+  constexpr int KR = RH <= 2 ? HD / 8 : 1;
+  x8 kv[KR];
+  if constexpr (RH <= 2) {
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c) kv[c] = fa::ld8(krow + 8 * c);
+  }
+  // V rows in flight per lane: all 64 for 1-2 heads per workgroup; with 4-8
+  // heads (GQA / MQA slices) the score / P.V registers leave room for 8
+  constexpr int VU = RH <= 2 ? 64 : 8;
+  vpair vv[VU];
+  const T* vbase = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + HP * lane;
+  auto load_v = [&](int u0) {
+#pragma unroll
+    for (int u = 0; u < VU; ++u) {
+      const int kc = min(k0 + wave * 64 + u0 + u, k0 + nk - 1);
+      vv[u] = *reinterpret_cast<const vpair*>(vbase + (int64_t)kc * p.v_ss);
+    }
+  };
+  load_v(0);
   // query vectors of this slice -> LDS (fp32)
   for (int i = tid; i < RH * HD; i += 256) {
     const int j = i / HD, d = i % HD;
@@ -87,18 +122,18 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   __syncthreads();
 
   // scores: lane = key
-  const int key = k0 + tid;
   float s[RH];
 #pragma unroll
   for (int j = 0; j < RH; ++j) s[j] = 0.f;
-  if (tid < nk) {
-    const T* krow = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)key * p.k_ss + (int64_t)g * p.k_sg;
+  if (RH <= 2 || tid < nk) {  // (the branch also bounds hipcc's hoisting of the query reads)
 #pragma unroll
     for (int c = 0; c < HD / 8; ++c) {
-      const typename fa::MT<T>::x8 kv = fa::ld8(krow + 8 * c);
+      x8 kc8;
+      if constexpr (RH <= 2) kc8 = kv[c];
+      else kc8 = fa::ld8(krow + 8 * c);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float kf = (float)kv[e];
+        const float kf = (float)kc8[e];
 #pragma unroll
         for (int j = 0; j < RH; ++j) s[j] = __builtin_fmaf(kf, qs[j][8 * c + e], s[j]);
       }
@@ -129,33 +164,25 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
   }
   __syncthreads();
 
-  // P.V: wave w takes keys w*64 .. w*64+63 of the chunk, lane = head-dim pair
+  // P.V: wave w takes keys w*64 .. w*64+63 of the chunk (p = 0 past the length)
   float acc[RH][HP];
 #pragma unroll
   for (int j = 0; j < RH; ++j)
 #pragma unroll
     for (int e = 0; e < HP; ++e) acc[j][e] = 0.f;
-  const T* vbase = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg + HP * lane;
-  const int kend = min(64, nk - wave * 64);
-  constexpr int U = 8;  // rows in flight per lane
-  for (int kk0 = 0; kk0 < kend; kk0 += U) {
-    float vf[U][HP];
+#pragma unroll 1
+  for (int u0 = 0; u0 < 64; u0 += VU) {
+    if (u0 > 0) load_v(u0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kc = wave * 64 + min(kk0 + u, kend - 1);
-      const T* vr = vbase + (int64_t)(k0 + kc) * p.v_ss;
+    for (int u = 0; u < VU; ++u) {
+      const int kc = wave * 64 + u0 + u;
 #pragma unroll
-      for (int e = 0; e < HP; ++e) vf[u][e] = (float)vr[e];
-    }
+      for (int j = 0; j < RH; ++j) {
+        const float pj = ps[j][kc];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (kk0 + u < kend) {
-        const int kc = wave * 64 + kk0 + u;
-#pragma unroll
-        for (int j = 0; j < RH; ++j) {
-          const float pj = ps[j][kc];
-#pragma unroll
-          for (int e = 0; e < HP; ++e) acc[j][e] = __builtin_fmaf(pj, vf[u][e], acc[j][e]);
+        for (int e = 0; e < HP; ++e) {
+          const uint16_t bits = (uint16_t)(vv[u] >> (16 * e));
+          acc[j][e] = __builtin_fmaf(pj, (float)__builtin_bit_cast(T, bits), acc[j][e]);
         }
       }
     }
@@ -166,8 +193,17 @@ __global__ __launch_bounds__(256) void decode_partial_k(const DecodeParams p) {
     for (int e = 0; e < HP; ++e) pacc[wave][j][HP * lane + e] = acc[j][e];
   __syncthreads();
 
+  if (nsplit == 1) {  // one chunk holds every key: normalise and write O here (no combine pass)
+    for (int i = tid; i < nh * HD; i += 256) {
+      const int j = i / HD, d = i % HD;
+      const int head = g * r + h0 + j;
+      const float l = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+      const float o = pacc[0][j][d] + pacc[1][j][d] + pacc[2][j][d] + pacc[3][j][d];
+      ((T*)p.o)[(int64_t)b * p.o_sb + (int64_t)head * p.o_sh + d] = (T)(l > 0.f ? o / l : 0.f);
+    }
+    return;
+  }
   // partial outputs: [b][nq][split][HD] plus (max, sum) per (b, head, split)
-  const int nsplit = gridDim.x;
   for (int i = tid; i < nh * HD; i += 256) {
     const int j = i / HD, d = i % HD;
     const int head = g * r + h0 + j;
@@ -224,6 +260,7 @@ void launch(const DecodeParams& p, hipStream_t s) {
   else if (r >= 4) launch_partial<T, HD, 4>(p, nsplit, s);
   else if (r >= 2) launch_partial<T, HD, 2>(p, nsplit, s);
   else launch_partial<T, HD, 1>(p, nsplit, s);
+  if (nsplit == 1) return;  // the partial kernel wrote O
   const int64_t total = (int64_t)p.b * p.nq * (HD / 4);
   hipLaunchKernelGGL((decode_combine_k<T, HD>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      s, p, nsplit);
