@@ -22,20 +22,28 @@ What makes the step capturable: nothing in it depends on the step on the host.
     ``ForwardStep`` and so by the text-generation API and server): only the
     forward is replayed, sampling and stop conditions stay eager.
 
+Tensor parallelism: every TP rank captures its own graph of the same step;
+the row-parallel all-reduces (two [b, h] sums per layer in the fused decode
+layer, ``models/transformer.py``) and the vocab all-gather of the logits are
+RCCL collectives recorded into the graph (RCCL kernels are capturable; the
+communicator is created by the eager warm-up forward, before capture, and the
+collective layer records no timing events while capturing).  All TP ranks run
+the generation loop in lockstep, as the reference's TP generation does
+(``megatron/text_generation/generation.py:179-264``), so every replay issues
+the same collective sequence on every rank.  Pipeline parallelism stays eager
+(a step is a chain of stage-to-stage sends across ranks).
+
 The reference decodes eagerly (``megatron/text_generation/generation.py``
 drives ``forward_step.py`` once per token); this is an MI355X-side addition.
-Single model-parallel rank (TP = PP = 1) only: the graph holds no collectives.
 """
 import torch
 
 from ..parallel import state
 
 
-def _check_single_rank():
-    if state.model_parallel_is_initialized() and (
-            state.get_tensor_model_parallel_world_size() > 1
-            or state.get_pipeline_model_parallel_world_size() > 1):
-        raise NotImplementedError("hipGraph decode runs on a single model-parallel rank")
+def _check_supported():
+    if state.model_parallel_is_initialized() and state.get_pipeline_model_parallel_world_size() > 1:
+        raise NotImplementedError("hipGraph decode runs without pipeline parallelism (PP = 1)")
     if not torch.cuda.is_available():
         raise RuntimeError("hipGraph decode needs a GPU")
 
@@ -43,8 +51,7 @@ def _check_single_rank():
 def graph_decode_supported():
     return torch.cuda.is_available() and (
         not state.model_parallel_is_initialized()
-        or (state.get_tensor_model_parallel_world_size() == 1
-            and state.get_pipeline_model_parallel_world_size() == 1))
+        or state.get_pipeline_model_parallel_world_size() == 1)
 
 
 class GraphedDecodeForward:
@@ -56,7 +63,7 @@ class GraphedDecodeForward:
     valid until the next call."""
 
     def __init__(self, model, inference_params, batch):
-        _check_single_rank()
+        _check_supported()
         self.model = model
         self.ip = inference_params
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -105,7 +112,7 @@ class GraphedGreedyDecoder:
     """
 
     def __init__(self, model, inference_params, batch, max_new_tokens):
-        _check_single_rank()
+        _check_supported()
         self.model = model
         self.ip = inference_params
         self.batch = batch

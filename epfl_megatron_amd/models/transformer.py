@@ -436,7 +436,8 @@ class ParallelTransformerLayer(MegatronModule):
                 and hasattr(self.input_layernorm, "forward_residual"))
 
     def _decode_fused_ok(self, hidden_states, ip):
-        """One decode step of a plain pre-RMSNorm rotary GLU block on one TP rank."""
+        """One decode step of a plain pre-RMSNorm rotary GLU block (any TP size,
+        no sequence parallelism: a decode step has one row per sequence)."""
         if not (_DECODE_FUSED and ip is not None and not torch.is_grad_enabled()
                 and hidden_states.is_cuda and hidden_states.dim() == 3
                 and hidden_states.shape[0] == 1 and hidden_states.shape[1] <= 16
@@ -450,7 +451,8 @@ class ParallelTransformerLayer(MegatronModule):
                 and sa.position_embedding_type == PositionEmbeddingType.rotary
                 and sa.query_key_value.bias is None and sa.dense.bias is None
                 and mlp.glu_activation and not mlp.use_bias
-                and state.get_tensor_model_parallel_world_size() == 1
+                and not sa.dense.sequence_parallel_enabled
+                and not mlp.dense_4h_to_h.sequence_parallel_enabled
                 and sa.hidden_size_per_attention_head in (64, 128)):
             return False
         C = ext()
@@ -495,10 +497,18 @@ class ParallelTransformerLayer(MegatronModule):
         else:
             o = flash_attn_func(q4, kc[:s0 + 1].transpose(0, 1), vc[:s0 + 1].transpose(0, 1),
                                 causal=True)
-        h2 = C.skinny_norm_gemm(o.reshape(b, -1), sa.dense.weight, None, 0.0, x)
+        # Row-parallel dense / fc2 under TP: each rank's product is a partial
+        # sum; TP rank 0 alone adds the residual in its epilogue, so one
+        # all-reduce of [b, H] yields partial sums + residual (reference
+        # RowParallelLinear + bias-dropout-add: megatron/model/transformer.py:
+        # 707-730, megatron/core/tensor_parallel/layers.py:665-701).
+        first = state.get_tensor_model_parallel_rank() == 0
+        h2 = C.skinny_norm_gemm(o.reshape(b, -1), sa.dense.weight, None, 0.0, x if first else None)
+        h2 = tp.reduce_from_tensor_model_parallel_region(h2)
         y = C.skinny_norm_glu(h2, mlp.dense_h_to_4h.weight, ln2.weight, ln2.eps,
                               tp.layers._GLU_KIND[mlp.glu_activation])
-        h3 = C.skinny_norm_gemm(y, mlp.dense_4h_to_h.weight, None, 0.0, h2)
+        h3 = C.skinny_norm_gemm(y, mlp.dense_4h_to_h.weight, None, 0.0, h2 if first else None)
+        h3 = tp.reduce_from_tensor_model_parallel_region(h3)
         return h3.view(1, b, H)
 
     def _forward_fused_residual(self, hidden_states, attention_mask, inference_params,

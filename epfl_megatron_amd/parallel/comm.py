@@ -88,7 +88,9 @@ def _account(key, nbytes):
 
 
 def _events_on(t):
-    return _TIMING[0] and t.is_cuda
+    # (no timing events inside a hipGraph capture: collectives of a captured
+    # TP decode step, inference/hip_graph.py)
+    return _TIMING[0] and t.is_cuda and not torch.cuda.is_current_stream_capturing()
 
 
 def _fold_events(block=False):

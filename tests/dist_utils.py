@@ -5,6 +5,7 @@ torchrun-style env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR=127.0.0.1), calls
 ``fn(rank, world_size, *args)`` in each and re-raises the first failure.
 Results are returned through a multiprocessing queue (``fn`` return values).
 """
+import io
 import os
 import socket
 import traceback
@@ -30,7 +31,12 @@ def _worker(rank, world, port, fn, args, q, env=None):
     torch.set_num_threads(1)
     try:
         out = fn(rank, world, *args)
-        q.put((rank, "ok", out))
+        # results travel as bytes, not as shared-memory tensors: a tensor put on
+        # the queue is backed by a segment the exiting worker may already have
+        # released when the parent unpickles it (FileNotFoundError)
+        buf = io.BytesIO()
+        torch.save(out, buf)
+        q.put((rank, "ok", buf.getvalue()))
     except Exception:  # pragma: no cover - reported to the parent
         q.put((rank, "err", traceback.format_exc()))
     finally:
@@ -58,7 +64,9 @@ def run_dist(fn, world_size, *args, timeout=600, env=None):
     for _ in range(world_size):
         rank, status, payload = q.get()
         if status == "ok":
-            results[rank] = payload
+            import torch
+            # (bytes written by this harness's own worker above)
+            results[rank] = torch.load(io.BytesIO(payload), weights_only=False)
         else:
             errors.append(f"rank {rank}:\n{payload}")
             break

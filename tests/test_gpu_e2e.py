@@ -297,3 +297,80 @@ def test_gpu_generation_api_hip_graph_matches_eager():
     assert graph_tokens == eager_tokens
     for a, b in zip(graph_lp, eager_lp):
         assert a == pytest.approx(b, abs=1e-2)
+
+
+def _decode_tp(rank, world, fused):
+    """KV-cached greedy decode of the tiny GQA Llama at TP = world on one GPU
+    (gloo collectives on cuda tensors: RCCL refuses two ranks on one device),
+    through the fused decode layer (``fused``) or the unfused kernels.
+    Returns the full-vocabulary decode logits and tokens."""
+    import torch.distributed as dist
+    import finetune
+    init_framework(LLAMA_GQA + ["--bf16", "--tensor_model_parallel_size", str(world)],
+                   finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType, transformer
+    from epfl_megatron_amd.training import get_model
+    from epfl_megatron_amd.inference.forward_step import InferenceParams
+    from epfl_megatron_amd.parallel import state
+    args = get_args()
+    model = get_model(finetune.model_provider, ModelType.encoder_or_decoder, wrap_with_ddp=False)
+    _deterministic_init(model, args)
+    m = model[0].eval()
+    transformer._DECODE_FUSED = fused
+    calls = [0]
+    orig = transformer.ParallelTransformerLayer._forward_decode_fused
+
+    def counted(self, *a, **k):
+        calls[0] += 1
+        return orig(self, *a, **k)
+    transformer.ParallelTransformerLayer._forward_decode_fused = counted
+
+    def full(lg):  # vocab-parallel logits -> all columns
+        if world == 1:
+            return lg
+        parts = [torch.empty_like(lg) for _ in range(world)]
+        dist.all_gather(parts, lg.contiguous(), group=state.get_tensor_model_parallel_group())
+        return torch.cat(parts, -1)
+    torch.manual_seed(6)
+    b, plen, n = 2, 17, 6
+    prompt = torch.randint(0, 512, (b, plen)).cuda()
+    pos = torch.arange(plen + n, device="cuda")[None].expand(b, -1)
+    with torch.no_grad():
+        ip = InferenceParams(b, plen + n)
+        nxt = full(m(prompt, pos[:, :plen], None, inference_params=ip))[:, -1].argmax(-1, keepdim=True)
+        ip.sequence_len_offset += plen
+        logits, toks = [], []
+        for t in range(plen, plen + n):
+            lg = full(m(nxt, pos[:, t:t + 1], None, inference_params=ip)).float()
+            nxt = lg[:, -1].argmax(-1, keepdim=True)
+            logits.append(lg.cpu())
+            toks.append(nxt.cpu())
+            ip.sequence_len_offset += 1
+    transformer._DECODE_FUSED = True
+    transformer.ParallelTransformerLayer._forward_decode_fused = orig
+    return calls[0], torch.cat(logits, 1), torch.cat(toks, 1).tolist()
+
+
+@pytest.mark.gpu
+def test_gpu_fused_decode_tensor_parallel():
+    """The fused decode layer at TP=2 (row-parallel partial sums, residual
+    added by TP rank 0 only, one all-reduce per row-parallel product) equals
+    the TP=1 fused decode and the TP=2 unfused decode: logits and tokens."""
+    c1, l1, t1 = run_dist(_decode_tp, 1, True)[0]
+    res = run_dist(_decode_tp, 2, True, env={"LOCAL_RANK": "0"})
+    c2, l2, t2 = res[0]
+    _, l2u, t2u = run_dist(_decode_tp, 2, False, env={"LOCAL_RANK": "0"})[0]
+    assert c1 == 2 * 6 and c2 == 2 * 6, (c1, c2)
+    scale = float(l1.abs().max())
+    tol = 3e-2 * max(1.0, scale)
+    assert float((l2 - l1).abs().max()) < tol
+    assert float((l2 - l2u).abs().max()) < tol
+    # greedy tokens agree except where the TP=1 logits of the two candidates
+    # are within the bf16 tolerance of each other (a near tie)
+    for tt in (t2, t2u):
+        for i, (ra, rb) in enumerate(zip(t1, tt)):
+            for j, (a, bb) in enumerate(zip(ra, rb)):
+                if a != bb:
+                    gap = float(l1[i, j, a] - l1[i, j, bb])
+                    assert abs(gap) < 2 * tol, (i, j, a, bb, gap)
