@@ -265,13 +265,10 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
 //     the next block's first U k-steps, so the stream never drains;
 //   * per block, the 8 partial tiles meet in a double-buffered LDS slot and
 //     wave 0 runs the epilogue while the other waves stream the next block.
-#ifndef SKINNY_PU
-#define SKINNY_PU 8
-#endif
-template <typename T, bool NORM, int EPI, int ACT, int STEPS>
+template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U>
 __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
-  constexpr int WAVES = 8, U = SKINNY_PU;
+  constexpr int WAVES = 8;
   static_assert(STEPS % U == 0, "ring must tile the k-steps");
   __shared__ f4 part[2][WAVES][64];
   __shared__ float ssq[WAVES][16];
@@ -396,9 +393,19 @@ void launch(const SkinnyArgs& p, hipStream_t s) {
     hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT>), dim3((unsigned)nblocks),
                        dim3(64 * WAVES), 0, s, p);
   } else {
+    // ring depth (k-steps of weight loads in flight per wave): 16 (batch-1 graph decode
+    // 301 -> 308 tok/s over 8, profiles/r3s_skinny_ring_depth.txt); EMA_SKINNY_PU=8 for A/B
+    static const int pu = [] {
+      const char* e = getenv("EMA_SKINNY_PU");
+      return e ? atoi(e) : 16;
+    }();
     const int g = nblocks < num_cus() ? nblocks : num_cus();
-    hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS>), dim3((unsigned)g), dim3(512), 0,
-                       s, p);
+    if (pu == 16)
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16>), dim3((unsigned)g), dim3(512),
+                         0, s, p);
+    else
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 8>), dim3((unsigned)g), dim3(512),
+                         0, s, p);
   }
 }
 
