@@ -208,6 +208,9 @@ FLAG_TABLE = {
         _flag("--tensor_model_parallel_size", type=int, default=1),
         _flag("--pipeline_model_parallel_size", type=int, default=1),
         _flag("--pipeline_model_parallel_split_rank", type=int, default=None),
+        _flag("--context_parallel_size", type=int, default=1,
+              help="MI355X addition: split every sequence over this many consecutive DP "
+                   "ranks; attention runs as a ring over them (parallel/context.py)"),
         _flag("--num_layers_per_virtual_pipeline_stage", type=int, default=None),
         _flag("--distributed_backend", default="nccl", choices=["nccl", "gloo"]),
         _flag("--DDP_impl", default="local", choices=["local", "torch"]),
@@ -377,11 +380,17 @@ def _derive_parallel_sizes(args):
              f"world size is not divisible by tensor parallel size "
              f"({args.tensor_model_parallel_size}) times pipeline parallel size "
              f"({args.pipeline_model_parallel_size})")
-    args.data_parallel_size = args.world_size // mp
+    cp = getattr(args, "context_parallel_size", 1) or 1
+    _require(args.world_size % (mp * cp) == 0,
+             f"world size ({args.world_size}) is not divisible by tp x pp ({mp}) times "
+             f"context parallel size ({cp})")
+    # data_parallel_size counts the ranks that read DIFFERENT samples (batch
+    # accounting); gradients are reduced over data_parallel_size x cp ranks.
+    args.data_parallel_size = args.world_size // mp // cp
     _log0(args, f"using world size: {args.world_size}, data-parallel-size: "
                 f"{args.data_parallel_size}, tensor-model-parallel size: "
                 f"{args.tensor_model_parallel_size}, pipeline-model-parallel size: "
-                f"{args.pipeline_model_parallel_size} ")
+                f"{args.pipeline_model_parallel_size}, context-parallel size: {cp} ")
     if args.pipeline_model_parallel_size > 1 and args.pipeline_model_parallel_split_rank is not None:
         _require(args.pipeline_model_parallel_split_rank < args.pipeline_model_parallel_size,
                  "split rank needs to be less than pipeline model parallel size")
@@ -553,6 +562,14 @@ def _derive_recompute_and_parallel_features(args):
         args.sequence_parallel = False
     if args.sequence_parallel:
         args.async_tensor_model_parallel_allreduce = False
+    cp = getattr(args, "context_parallel_size", 1) or 1
+    if cp > 1:
+        _require(args.seq_length % cp == 0,
+                 f"seq_length ({args.seq_length}) is not divisible by context parallel "
+                 f"size ({cp})")
+        _require(not args.reset_attention_mask,
+                 "--reset_attention_mask is not supported with context parallelism")
+        _require(not sim_tp, "--simulated_tensor_parallel_size excludes context parallelism")
     # Reference defect D17: the GQA view silently breaks when KV heads do not
     # split evenly over TP ranks; we check it explicitly.
     if args.num_attention_heads_kv % (sim_tp or args.tensor_model_parallel_size) != 0:

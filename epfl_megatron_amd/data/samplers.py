@@ -17,8 +17,9 @@ def build_pretraining_data_loader(dataset, consumed_samples):
     if dataset is None:
         return None
     args = global_vars.get_args()
-    dp_rank = state.get_data_parallel_rank()
-    dp_size = state.get_data_parallel_world_size()
+    # context-parallel ranks of one DP group read the same samples
+    dp_rank = state.get_data_sample_parallel_rank()
+    dp_size = state.get_data_sample_parallel_world_size()
     if args.dataloader_type == "single":
         sampler = MegatronPretrainingSampler(len(dataset), consumed_samples, args.micro_batch_size,
                                              dp_rank, dp_size)

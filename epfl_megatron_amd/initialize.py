@@ -106,7 +106,8 @@ def _initialize_distributed(args):
                                         args.pipeline_model_parallel_size,
                                         args.virtual_pipeline_model_parallel_size,
                                         args.pipeline_model_parallel_split_rank,
-                                        getattr(args, "ddp_comm_groups", 1))
+                                        getattr(args, "ddp_comm_groups", 1),
+                                        getattr(args, "context_parallel_size", 1))
     sim_tp = getattr(args, "simulated_tensor_parallel_size", None)
     if sim_tp and sim_tp > 1:
         # one rank (rank 0) of a TP=sim_tp model; TP collectives loop back locally

@@ -34,6 +34,7 @@ from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync
 from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
 from ..ops._ext import use_native, ext
+from ..parallel.context import chunk_position_ids, ring_attention
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
 from ..ops.activations import glu, bias_gelu, gelu
 from ..ops.softmax import FusedScaleMaskSoftmax
@@ -251,6 +252,9 @@ class ParallelAttention(MegatronModule):
         self.position_embedding_type = args.position_embedding_type
         self.rope_len = max(args.seq_length, args.max_position_embeddings or 0)
         self.rope_scaling = args.rope_scaling_factor
+        # context parallelism: this rank holds one contiguous sequence chunk
+        self.cp_group = state.get_context_parallel_group() \
+            if attention_type == AttnType.self_attn else None
 
     # -- helpers ---------------------------------------------------------
     def _rope(self, device):
@@ -294,6 +298,8 @@ class ParallelAttention(MegatronModule):
         if inference_params is not None:
             ctx = self._inference_forward(mixed, attention_mask, inference_params, position_ids,
                                           rope)
+        elif self.cp_group is not None:
+            ctx = self._context_parallel_forward(mixed, position_ids, rope)
         elif self.use_flash_attn:
             rng = tp.get_cuda_rng_tracker().fork() if not self.sequence_parallel else nullcontext()
             with rng:
@@ -311,6 +317,21 @@ class ParallelAttention(MegatronModule):
                 k = apply_rope_ref(k, rope[0], rope[1], position_ids)
             ctx = self._core(q, self._expand_kv(k), self._expand_kv(v), attention_mask)
         return self.dense(ctx)
+
+    def _context_parallel_forward(self, mixed, position_ids, rope):
+        """Causal self-attention of this rank's chunk over the whole sequence:
+        RoPE at the chunk's global positions, then the K/V ring
+        (``parallel/context.py``) with the FlashAttention pair kernels."""
+        sq, b = mixed.shape[:2]
+        q, k, v = self._split_qkv(mixed)
+        if rope is not None:
+            if position_ids is None:
+                position_ids = chunk_position_ids(sq, b, mixed.device)
+            q = apply_rope_ref(q, rope[0], rope[1], position_ids)
+            k = apply_rope_ref(k, rope[0], rope[1], position_ids)
+        o = ring_attention(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1),
+                           self.cp_group, causal=True)
+        return o.transpose(0, 1).reshape(sq, b, -1)
 
     def _inference_forward(self, mixed, attention_mask, ip, position_ids, rope):
         s0 = ip.sequence_len_offset

@@ -27,6 +27,14 @@ The per-pair kernels are the training kernels (``csrc/flash_attn_fwd.hip`` /
 same math runs in fp32 torch (tests, gloo).  ``ring_attention_simulated`` runs
 the W ranks of a ring one after another in one process (kernel-level tests on
 one GPU).
+
+Training integration (``--context_parallel_size C``): C consecutive DP ranks
+form a context-parallel group (``state.get_context_parallel_group``) and read
+the same samples; ``get_batch_on_this_cp_rank`` keeps this rank's contiguous
+sequence chunk (global position ids included), self-attention runs
+``ring_attention`` (``models/transformer.py``), and ``cp_token_mean`` makes the
+per-rank loss the exact whole-sequence token mean once DDP averages gradients
+over all DP x CP ranks.
 """
 import math
 
@@ -232,3 +240,43 @@ def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_o
                 dks[j] += dk
                 dvs[j] += dv
     return outs, (dqs, dks, dvs)
+
+
+# ---------------------------------------------------------------------------
+# training integration
+# ---------------------------------------------------------------------------
+def get_batch_on_this_cp_rank(tensors, dim=1):
+    """This rank's contiguous chunk (along the sequence ``dim``) of every tensor."""
+    from . import state
+    C = state.get_context_parallel_world_size()
+    if C == 1:
+        return tensors
+    r = state.get_context_parallel_rank()
+    out = []
+    for t in tensors:
+        if t is None or not torch.is_tensor(t) or t.dim() <= dim:
+            out.append(t)
+            continue
+        c = t.shape[dim] // C
+        out.append(t.narrow(dim, r * c, c).contiguous())
+    return out
+
+
+def cp_token_mean(losses, loss_mask):
+    """Masked token mean of the local chunk's ``losses`` scaled so that the DP
+    average over the C ranks of a sequence is the whole sequence's mean:
+    ``C * sum(local) / sum(mask over the group)``."""
+    from . import state
+    group = state.get_context_parallel_group()
+    if group is None:
+        return torch.sum(losses * loss_mask) / loss_mask.sum()
+    n = loss_mask.sum().detach().clone()
+    comm.all_reduce(n, group=group)
+    return torch.sum(losses * loss_mask) * dist.get_world_size(group) / n
+
+
+def chunk_position_ids(s, b, device):
+    """Global positions of this rank's chunk ``[b, s]``."""
+    from . import state
+    r = state.get_context_parallel_rank()
+    return (r * s + torch.arange(s, device=device)).unsqueeze(0).expand(b, s)

@@ -160,7 +160,7 @@ def forward_backward_no_pipelining(forward_step_func, data_iterator, model, opti
 
 def get_tensor_shapes(rank, model_type):
     args = global_vars.get_args()
-    seq = args.seq_length
+    seq = args.seq_length // state.get_context_parallel_world_size()
     if args.sequence_parallel:
         seq = seq // state.get_tensor_model_parallel_world_size()
     if model_type == ModelType.encoder_and_decoder:
@@ -308,7 +308,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func, data_iterat
     if m % pp != 0:
         raise RuntimeError(f"number of microbatches ({m}) is not divisible by pipeline-model-"
                            f"parallel size ({pp}) when using interleaved schedule")
-    seq = args.seq_length
+    seq = args.seq_length // state.get_context_parallel_world_size()
     if args.sequence_parallel:
         seq //= state.get_tensor_model_parallel_world_size()
     shape = (seq, args.micro_batch_size, args.hidden_size)

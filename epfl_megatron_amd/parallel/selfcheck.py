@@ -106,6 +106,10 @@ def collective_selfcheck(verbose=True):
     n += _check_group("tp", state.get_tensor_model_parallel_group(),
                       state.get_tensor_model_parallel_world_size(),
                       state.get_tensor_model_parallel_rank(), dev)
+    if state.get_context_parallel_group() is not None:
+        n += _check_group("cp", state.get_context_parallel_group(),
+                          state.get_context_parallel_world_size(),
+                          state.get_context_parallel_rank(), dev)
     n += _check_pipeline(dev)
     comm.report(reset=True)  # keep the check out of the training accounting
     if verbose:
@@ -113,5 +117,6 @@ def collective_selfcheck(verbose=True):
         if dist.get_rank() == 0:
             print(f"> collective self-check passed ({n} checks; dp={state.get_data_parallel_world_size()}"
                   f" x{len(dp_groups)} comm groups, tp={state.get_tensor_model_parallel_world_size()}, "
-                  f"pp={state.get_pipeline_model_parallel_world_size()})", flush=True)
+                  f"pp={state.get_pipeline_model_parallel_world_size()}, "
+                  f"cp={state.get_context_parallel_world_size()})", flush=True)
     return n

@@ -35,6 +35,9 @@ class _State:
     # extra communicators over the same DP ranks (one RCCL stream each)
     dp_comm_groups: List[object] = field(default_factory=list)
     tp_global_ranks: List[int] = field(default_factory=list)
+    # context parallelism: consecutive DP indices share one sequence
+    cp_group: Optional[object] = None
+    cp_size: int = 1
     virtual_pp_rank: Optional[int] = None
     virtual_pp_world_size: Optional[int] = None
     pp_split_rank: Optional[int] = None
@@ -66,7 +69,8 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
                               pipeline_model_parallel_size=1,
                               virtual_pipeline_model_parallel_size=None,
                               pipeline_model_parallel_split_rank=None,
-                              data_parallel_comm_groups=1):
+                              data_parallel_comm_groups=1,
+                              context_parallel_size=1):
     """Create TP/DP/PP/model-parallel/embedding groups.
 
     Every rank must call ``new_group`` for every group in the same order
@@ -74,6 +78,11 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
     ``data_parallel_comm_groups`` > 1 adds communicators over the same DP ranks:
     each has its own RCCL stream, so the DDP buckets assigned round-robin to
     them are reduced concurrently.
+    ``context_parallel_size`` C > 1 subdivides every DP group: C consecutive
+    DP indices (each TP / PP coordinate fixed) hold the C sequence chunks of
+    the same samples and form one context-parallel group (``parallel/context.py``
+    ring attention).  Gradients are still reduced over the whole DP group;
+    the data loader shards samples over DP / C.
     """
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed must be initialized first")
@@ -99,6 +108,18 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
             if rank in ranks:
                 _S.dp_group, _S.dp_global_ranks = g, [int(r) for r in ranks]
     _S.dp_comm_groups = [_S.dp_group]
+    cp = int(context_parallel_size or 1)
+    if ndp % cp != 0:
+        raise RuntimeError(f"data parallel size ({ndp}) is not divisible by context parallel "
+                           f"size ({cp})")
+    _S.cp_size = cp
+    for p in range(npp):
+        for t in range(ntp):
+            for c0 in range(0, ndp, cp):
+                ranks = grid[p, c0:c0 + cp, t]
+                g = _new_group(ranks) if cp > 1 else None
+                if rank in ranks:
+                    _S.cp_group = g
     for _ in range(max(1, int(data_parallel_comm_groups)) - 1):
         for p in range(npp):
             for t in range(ntp):
@@ -154,7 +175,7 @@ def initialize_model_parallel(tensor_model_parallel_size=1,
         comm.name_group(g, f"dp{i + 1}")
     for g, name in ((_S.dp_group, "dp"), (_S.mp_group, "mp"), (_S.tp_group, "tp"),
                     (_S.pp_group, "pp"), (_S.embedding_group, "emb"),
-                    (_S.position_embedding_group, "posemb")):
+                    (_S.position_embedding_group, "posemb"), (_S.cp_group, "cp")):
         if g is not None:
             comm.name_group(g, name)
 
@@ -265,6 +286,28 @@ def get_data_parallel_world_size():
 
 def get_data_parallel_rank():
     return _group_rank(_S.dp_group)
+
+
+def get_context_parallel_group():
+    """The ranks sharing one sequence (None when context parallelism is off)."""
+    return _S.cp_group
+
+
+def get_context_parallel_world_size():
+    return _S.cp_size if _S.cp_group is not None else 1
+
+
+def get_context_parallel_rank():
+    return _group_rank(_S.cp_group) if _S.cp_group is not None else 0
+
+
+def get_data_sample_parallel_world_size():
+    """Ranks that read different samples: DP / CP."""
+    return get_data_parallel_world_size() // get_context_parallel_world_size()
+
+
+def get_data_sample_parallel_rank():
+    return get_data_parallel_rank() // get_context_parallel_world_size()
 
 
 def get_virtual_pipeline_model_parallel_rank():

@@ -430,7 +430,7 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
         loss_dict, skipped_iter, grad_norm, num_zeros = train_step(
             forward_step_func, train_data_iterator, model, optimizer, opt_param_scheduler, args)
         iteration += 1
-        args.consumed_train_samples += state.get_data_parallel_world_size() * \
+        args.consumed_train_samples += args.data_parallel_size * \
             args.micro_batch_size * step_microbatches
         # Log the PREVIOUS iteration now that this one is enqueued: reading its
         # loss / grad norm / skip flag then never stalls the GPU queue.
@@ -515,7 +515,7 @@ def evaluate(forward_step_func, data_iterator, model, process_non_loss_data_func
                 for ld in losses:
                     for k, v in ld.items():
                         total[k] = total.get(k, 0.0) + v
-            args.consumed_valid_samples += state.get_data_parallel_world_size() * \
+            args.consumed_valid_samples += args.data_parallel_size * \
                 args.micro_batch_size * get_num_microbatches()
         collected = None
         if process_non_loss_data_func is not None and state.is_pipeline_last_stage():

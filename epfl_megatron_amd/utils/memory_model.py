@@ -34,7 +34,7 @@ def _tp(args):
 
 def layer_activation_bytes(args, micro_batch=None):
     """Bytes one transformer layer saves for the backward, per micro-batch."""
-    s = args.seq_length
+    s = args.seq_length // (getattr(args, "context_parallel_size", 1) or 1)
     b = micro_batch or args.micro_batch_size
     tp = _tp(args)
     h = args.hidden_size
@@ -60,7 +60,8 @@ def layer_activation_bytes(args, micro_batch=None):
 def static_bytes(args, n_params_rank):
     """Weights, gradients, optimizer state and the W^T cache of one GPU."""
     el = 2 if (args.bf16 or args.fp16) else 4
-    dp = args.data_parallel_size if args.use_distributed_optimizer else 1
+    dp = args.data_parallel_size * (getattr(args, "context_parallel_size", 1) or 1) \
+        if args.use_distributed_optimizer else 1
     weights = n_params_rank * el
     grads = n_params_rank * 4 if args.accumulate_allreduce_grads_in_fp32 or el == 2 else 0
     master = n_params_rank * 4 / dp if el == 2 else 0
@@ -74,7 +75,7 @@ def estimate(args, n_params_rank, layers, recomputed, in_flight=1):
     pipeline stage) recomputed and ``in_flight`` micro-batches live."""
     act = layer_activation_bytes(args)
     tp = _tp(args)
-    t = args.seq_length * args.micro_batch_size
+    t = args.seq_length // (getattr(args, "context_parallel_size", 1) or 1) * args.micro_batch_size
     t_res = t // tp if args.sequence_parallel else t
     inp = t_res * args.hidden_size * (2 if (args.bf16 or args.fp16) else 4)
     per_mb = (layers - recomputed) * act + recomputed * inp

@@ -14,6 +14,7 @@ from epfl_megatron_amd import get_args, get_tokenizer, get_timers, print_rank_0
 from epfl_megatron_amd.initialize import initialize_megatron
 from epfl_megatron_amd.models import FalconModel, GPTModel, LlamaModel, ModelType
 from epfl_megatron_amd.parallel import tensor as tensor_parallel
+from epfl_megatron_amd.parallel.context import cp_token_mean, get_batch_on_this_cp_rank
 from epfl_megatron_amd.training import pretrain
 from epfl_megatron_amd.utils.misc import (average_losses_across_data_parallel_group,
                                           get_ltor_masks_and_position_ids)
@@ -53,13 +54,18 @@ def get_batch(data_iterator):
     attention_mask, loss_mask, position_ids = get_ltor_masks_and_position_ids(
         tokens, tokenizer.eod, args.reset_position_ids, args.reset_attention_mask,
         args.eod_mask_loss, flash_doc_bounds=args.use_flash_attn)
+    if args.context_parallel_size > 1:
+        # this rank's sequence chunk; the causal mask is implied by the ring
+        tokens, labels, loss_mask, position_ids = get_batch_on_this_cp_rank(
+            [tokens, labels, loss_mask, position_ids])
+        attention_mask = None
     return tokens, labels, loss_mask, attention_mask, position_ids
 
 
 def loss_func(loss_mask, output_tensor):
     losses = output_tensor.float()
     loss_mask = loss_mask.view(-1).float()
-    loss = torch.sum(losses.view(-1) * loss_mask) / loss_mask.sum()
+    loss = cp_token_mean(losses.view(-1), loss_mask)
     averaged = average_losses_across_data_parallel_group([loss])
     return loss, {"lm loss": averaged[0]}
 
@@ -71,7 +77,7 @@ def forward_step(data_iterator, model):
     timers("batch-generator").stop()
     args = get_args()
     # RoPE position ids are only needed when they are not arange(s).
-    pos = position_ids if args.reset_position_ids else None
+    pos = position_ids if (args.reset_position_ids or args.context_parallel_size > 1) else None
     if args.position_embedding_type.name == "absolute":
         pos = position_ids
     output_tensor = model(tokens, pos, attention_mask, labels=labels)

@@ -835,3 +835,27 @@ def test_ring_attention_kernels(W, causal, nq, nkv, hd):
     _close(torch.cat(dqs, 1), qr.grad, 6e-2, 6e-2, "ring dq")
     _close(torch.cat(dks, 1), kr.grad, 6e-2, 6e-2, "ring dk")
     _close(torch.cat(dvs, 1), vr.grad, 6e-2, 6e-2, "ring dv")
+
+
+@pytest.mark.gpu
+def test_ring_pair_kernels_on_sequence_major_views():
+    """The model's context-parallel path hands the ring [s, b, n, d] tensors
+    transposed to [b, s, n, d] (models/transformer.py
+    _context_parallel_forward): the pair kernels read them through strides and
+    must match the contiguous layout bit for bit."""
+    from epfl_megatron_amd.parallel.context import _pair_bwd, _pair_fwd
+    torch.manual_seed(7)
+    s, b, nq, nkv, hd = 320, 2, 8, 2, 128
+    q = torch.randn(s, b, nq, hd, device=DEV, dtype=torch.bfloat16).transpose(0, 1)
+    k = torch.randn(s, b, nkv, hd, device=DEV, dtype=torch.bfloat16).transpose(0, 1)
+    v = torch.randn(s, b, nkv, hd, device=DEV, dtype=torch.bfloat16).transpose(0, 1)
+    do = torch.randn(s, b, nq, hd, device=DEV, dtype=torch.bfloat16).transpose(0, 1)
+    for causal in (True, False):
+        o1, l1 = _pair_fwd(q, k, v, causal, hd ** -0.5)
+        o2, l2 = _pair_fwd(q.contiguous(), k.contiguous(), v.contiguous(), causal, hd ** -0.5)
+        assert torch.equal(o1, o2) and torch.equal(l1, l2)
+        g1 = _pair_bwd(q, k, v, o1, l1, do, causal, hd ** -0.5)
+        g2 = _pair_bwd(q.contiguous(), k.contiguous(), v.contiguous(), o2, l2, do.contiguous(),
+                       causal, hd ** -0.5)
+        for a, c in zip(g1, g2):
+            assert torch.equal(a, c)

@@ -329,3 +329,44 @@ def test_llama_pp_distributed_optimizer():
     got = _losses(run_dist(_train, 4, TINY_LLAMA + _mb(1, 4) + [
         "--pipeline_model_parallel_size", "2", "--use_distributed_optimizer"], 3))
     _check(base, got)
+
+
+# --- context parallelism (--context_parallel_size): ring attention over
+# consecutive DP ranks that hold the sequence chunks of the same samples ---
+def test_llama_context_parallel(llama_ref):
+    got = _losses(run_dist(_train, 2, TINY_LLAMA + ["--context_parallel_size", "2",
+                                                     "--micro_batch_size", "2",
+                                                     "--global_batch_size", "4"], 3))
+    _check(llama_ref, got)
+
+
+def test_gpt_context_parallel_absolute_positions(gpt_ref):
+    """Learned absolute position embeddings read the chunk's GLOBAL positions."""
+    got = _losses(run_dist(_train, 2, TINY_GPT + ["--context_parallel_size", "2",
+                                                   "--micro_batch_size", "2",
+                                                   "--global_batch_size", "4"], 3))
+    _check(gpt_ref, got)
+
+
+def test_llama_context_parallel_gqa_eod_mask():
+    """GQA ring, and a loss mask that differs between the chunks (EOD tokens
+    masked): the CP-summed token count keeps the loss the whole-sequence mean."""
+    argv = TINY_LLAMA + ["--num_attention_heads_kv", "2", "--eod_mask_loss",
+                         "--micro_batch_size", "1", "--global_batch_size", "2"]
+    base = _losses(run_dist(_train, 1, argv, 3))
+    got = _losses(run_dist(_train, 4, argv + ["--context_parallel_size", "4"], 3))
+    _check(base, got)
+
+
+def test_llama_cp_tp_dp_pp():
+    """CP=2 composed with TP=2 + SP and DP=2 (8 ranks), and with PP=2 (4 ranks)."""
+    argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "4"]
+    base = _losses(run_dist(_train, 1, argv, 2))
+    got = _losses(run_dist(_train, 8, argv + ["--tensor_model_parallel_size", "2",
+                                              "--sequence_parallel",
+                                              "--context_parallel_size", "2",
+                                              "--use_distributed_optimizer"], 2))
+    _check(base, got, tol=5e-5)
+    got = _losses(run_dist(_train, 4, argv + ["--pipeline_model_parallel_size", "2",
+                                              "--context_parallel_size", "2"], 2))
+    _check(base, got, tol=5e-5)

@@ -65,3 +65,24 @@ def test_rank_grid_layout():
     g = rank_grid(16, 2, 4)
     assert g.shape == (4, 2, 2)
     assert g[1, 1, 0] == 1 * 4 + 1 * 2 + 0
+
+
+def _cp_topology(rank, world):
+    from epfl_megatron_amd.parallel import state
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    state.initialize_model_parallel(2, 1, context_parallel_size=2)
+    return (dist.get_process_group_ranks(state.get_context_parallel_group()),
+            state.get_context_parallel_rank(), state.get_data_sample_parallel_rank(),
+            state.get_data_sample_parallel_world_size(), state.get_data_parallel_world_size())
+
+
+def test_context_parallel_groups_tp2_cp2_dp2():
+    """grid [pp=1, dp=4, tp=2]: CP pairs consecutive DP indices, so rank r
+    shares its sequence with r +- tp; DP sample index = dp index // 2."""
+    res = run_dist(_cp_topology, 8)
+    for rank, (ranks, cpr, sr, ssize, dsize) in enumerate(res):
+        dp_idx, tp_idx = rank // 2, rank % 2
+        c0 = dp_idx // 2 * 2
+        assert ranks == [c0 * 2 + tp_idx, (c0 + 1) * 2 + tp_idx]
+        assert cpr == dp_idx % 2 and sr == dp_idx // 2
+        assert ssize == 2 and dsize == 4

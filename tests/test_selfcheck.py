@@ -20,6 +20,14 @@ def test_selfcheck_passes_on_3d_grid():
     assert counts == [19] * 8
 
 
+def test_selfcheck_passes_with_context_parallel():
+    argv = TINY_LLAMA + ["--tensor_model_parallel_size", "2", "--context_parallel_size", "2",
+                         "--micro_batch_size", "1", "--global_batch_size", "4"]
+    counts = run_dist(_init_and_count, 4, argv)
+    # DP (2 ranks) 6 + TP 6 + CP 6 (no pipeline)
+    assert counts == [18] * 4
+
+
 def _broken_avg(rank, world, argv):
     import finetune
     init_framework(argv + ["--no_comm_selfcheck"], finetune.extra_args)
