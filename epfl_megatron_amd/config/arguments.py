@@ -564,9 +564,9 @@ def _derive_recompute_and_parallel_features(args):
         args.async_tensor_model_parallel_allreduce = False
     cp = getattr(args, "context_parallel_size", 1) or 1
     if cp > 1:
-        _require(args.seq_length % cp == 0,
-                 f"seq_length ({args.seq_length}) is not divisible by context parallel "
-                 f"size ({cp})")
+        _require(args.seq_length % (2 * cp) == 0,
+                 f"seq_length ({args.seq_length}) is not divisible by 2 x context parallel "
+                 f"size ({cp}) (zig-zag sequence split)")
         _require(not args.reset_attention_mask,
                  "--reset_attention_mask is not supported with context parallelism")
         _require(not sim_tp, "--simulated_tensor_parallel_size excludes context parallelism")

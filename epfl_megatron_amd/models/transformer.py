@@ -319,9 +319,9 @@ class ParallelAttention(MegatronModule):
         return self.dense(ctx)
 
     def _context_parallel_forward(self, mixed, position_ids, rope):
-        """Causal self-attention of this rank's chunk over the whole sequence:
-        RoPE at the chunk's global positions, then the K/V ring
-        (``parallel/context.py``) with the FlashAttention pair kernels."""
+        """Causal self-attention of this rank's zig-zag share of the sequence
+        over the whole sequence: RoPE at the share's global positions, then the
+        K/V ring (``parallel/context.py``) with the FlashAttention pair kernels."""
         sq, b = mixed.shape[:2]
         q, k, v = self._split_qkv(mixed)
         if rope is not None:
@@ -330,7 +330,7 @@ class ParallelAttention(MegatronModule):
             q = apply_rope_ref(q, rope[0], rope[1], position_ids)
             k = apply_rope_ref(k, rope[0], rope[1], position_ids)
         o = ring_attention(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1),
-                           self.cp_group, causal=True)
+                           self.cp_group, causal=True, zigzag=True)
         return o.transpose(0, 1).reshape(sq, b, -1)
 
     def _inference_forward(self, mixed, attention_mask, ip, position_ids, rope):

@@ -28,10 +28,15 @@ same math runs in fp32 torch (tests, gloo).  ``ring_attention_simulated`` runs
 the W ranks of a ring one after another in one process (kernel-level tests on
 one GPU).
 
+Zig-zag layout: with a contiguous split the causal work grows with the rank
+(rank W-1 runs W pairs, rank 0 one).  Cutting the sequence into 2W pieces and
+giving rank r pieces r and 2W-1-r makes every off-diagonal pair exactly half
+a pair (``_plan``), so all ranks finish each ring step together.
+
 Training integration (``--context_parallel_size C``): C consecutive DP ranks
 form a context-parallel group (``state.get_context_parallel_group``) and read
-the same samples; ``get_batch_on_this_cp_rank`` keeps this rank's contiguous
-sequence chunk (global position ids included), self-attention runs
+the same samples; ``get_batch_on_this_cp_rank`` keeps this rank's zig-zag
+share of the sequence (global position ids included), self-attention runs
 ``ring_attention`` (``models/transformer.py``), and ``cp_token_mean`` makes the
 per-rank loss the exact whole-sequence token mean once DDP averages gradients
 over all DP x CP ranks.
@@ -118,11 +123,29 @@ def _merge(o, lse, o_j, lse_j):
     return o * w_old + o_j * w_new, new
 
 
-def _visible(j, r, causal):
-    """(run the pair?, causal kernel?) for chunk j against local queries of rank r."""
+def _plan(j, r, causal, zigzag):
+    """Which rows of the local Q and of K/V chunk j meet, and with which mask.
+
+    Returns None (pair fully masked) or (q_rows, kv_rows, causal_kernel) with
+    rows ``"all"``, ``"first"`` or ``"second"`` (halves of the chunk).
+    zig-zag layout (``zigzag=True``): rank r holds sequence pieces r and
+    2W-1-r of 2W, so for causal attention every off-diagonal pair is half a
+    pair (j < r: all queries see K/V piece j only; j > r: only the late query
+    piece sees both K/V pieces) and all ranks do the same work."""
     if not causal:
-        return True, False
-    return j <= r, j == r
+        return "all", "all", False
+    if j == r:
+        return "all", "all", True
+    if not zigzag:
+        return ("all", "all", False) if j < r else None
+    return ("all", "first", False) if j < r else ("second", "all", False)
+
+
+def _rows(t, which):
+    if which == "all":
+        return t
+    h = t.shape[1] // 2
+    return t[:, :h] if which == "first" else t[:, h:]
 
 
 # ---------------------------------------------------------------------------
@@ -148,9 +171,10 @@ class _Ring:
 
 class _RingAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, group, causal, scale):
+    def forward(ctx, q, k, v, group, causal, scale, zigzag):
         ring = _Ring(group)
         W, r = ring.world, ring.rank
+        h = q.shape[1] // 2
         o = lse = None
         kv = [k.contiguous(), v.contiguous()]
         for i in range(W):
@@ -158,16 +182,23 @@ class _RingAttnFn(torch.autograd.Function):
             work = recv = None
             if i + 1 < W:
                 work, recv = ring.shift(kv)  # next chunk in flight during this step
-            run, c = _visible(j, r, causal)
-            if run:
-                o_j, lse_j = _pair_fwd(q, kv[0], kv[1], c, scale)
-                o, lse = _merge(o, lse, o_j, lse_j)
+            plan = _plan(j, r, causal, zigzag)
+            if plan is not None:
+                qs, ks, c = plan
+                o_j, lse_j = _pair_fwd(_rows(q, qs), _rows(kv[0], ks), _rows(kv[1], ks), c,
+                                       scale)
+                if qs == "all":
+                    o, lse = _merge(o, lse, o_j, lse_j)
+                else:  # late query piece only (step 0 is the diagonal: o is set)
+                    o2, l2 = _merge(o[:, h:], lse[..., h:], o_j, lse_j)
+                    o = torch.cat([o[:, :h], o2], 1)
+                    lse = torch.cat([lse[..., :h], l2], -1)
             if work is not None:
                 work.wait()
                 kv = recv
         out = o.to(q.dtype)
         ctx.save_for_backward(q, k, v, out, lse)
-        ctx.group, ctx.causal, ctx.scale = group, causal, scale
+        ctx.group, ctx.causal, ctx.scale, ctx.zigzag = group, causal, scale, zigzag
         return out
 
     @staticmethod
@@ -183,33 +214,49 @@ class _RingAttnFn(torch.autograd.Function):
                torch.zeros(v.shape, dtype=torch.float32, device=v.device)]
         for i in range(W):
             j = (r - i) % W
-            run, c = _visible(j, r, ctx.causal)
-            if run:
-                dq_j, dk_j, dv_j = _pair_bwd(q, buf[0], buf[1], out, lse, dout, c, ctx.scale)
-                dq += dq_j
-                buf[2] = buf[2] + dk_j
-                buf[3] = buf[3] + dv_j
+            plan = _plan(j, r, ctx.causal, ctx.zigzag)
+            if plan is not None:
+                qs, ks, c = plan
+                dq_j, dk_j, dv_j = _pair_bwd(_rows(q, qs), _rows(buf[0], ks), _rows(buf[1], ks),
+                                             _rows(out, qs), lse if qs == "all" else
+                                             lse[..., q.shape[1] // 2:],
+                                             _rows(dout, qs), c, ctx.scale)
+                _rows(dq, qs).add_(dq_j)
+                _rows(buf[2], ks).add_(dk_j)
+                _rows(buf[3], ks).add_(dv_j)
             if W > 1:  # W hops bring every chunk back to its owner
                 work, recv = ring.shift(buf)
                 work.wait()
                 buf = recv
-        return dq.to(q.dtype), buf[2].to(k.dtype), buf[3].to(v.dtype), None, None, None
+        return (dq.to(q.dtype), buf[2].to(k.dtype), buf[3].to(v.dtype), None, None, None, None)
 
 
-def ring_attention(q, k, v, group, causal=True, softmax_scale=None):
+def ring_attention(q, k, v, group, causal=True, softmax_scale=None, zigzag=False):
     """Attention of the local query chunk over the whole sequence of ``group``.
 
-    q ``[b, s, nq, d]``, k / v ``[b, s, nkv, d]``: this rank's contiguous
-    sequence chunk (rank r of the group holds positions r*s .. r*s+s-1).
+    q ``[b, s, nq, d]``, k / v ``[b, s, nkv, d]``: this rank's sequence chunk,
+    contiguous (rank r of W holds positions r*s .. r*s+s-1) or, with
+    ``zigzag``, the pieces r and 2W-1-r of 2W (s/2 positions each, in that
+    order; ``zigzag_slice``), which balances causal work over the ranks.
     Returns ``[b, s, nq, d]``."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if group is None or dist.get_world_size(group) == 1:
         from ..ops.attention import flash_attn_func
         return flash_attn_func(q, k, v, causal=causal, softmax_scale=scale)
-    return _RingAttnFn.apply(q, k, v, group, causal, scale)
+    if zigzag and q.shape[1] % 2:
+        raise ValueError("zig-zag context parallelism needs an even local chunk")
+    return _RingAttnFn.apply(q, k, v, group, causal, scale, bool(zigzag))
 
 
-def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_outs=None):
+def zigzag_slice(t, dim, rank, world):
+    """Pieces ``rank`` and ``2*world-1-rank`` of ``2*world`` along ``dim``."""
+    n = t.shape[dim] // (2 * world)
+    return torch.cat([t.narrow(dim, rank * n, n),
+                      t.narrow(dim, (2 * world - 1 - rank) * n, n)], dim)
+
+
+def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_outs=None,
+                             zigzag=False):
     """The W ranks of a ring run one after another in one process (kernel
     tests on one GPU): ``qs`` / ``ks`` / ``vs`` are the per-rank chunks.
     Returns the per-rank outputs and, with ``grad_outs``, (dq, dk, dv) per rank."""
@@ -217,12 +264,20 @@ def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_o
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(qs[0].shape[-1])
     outs, lses = [], []
     for r in range(W):
+        h = qs[r].shape[1] // 2
         o = lse = None
         for i in range(W):
             j = (r - i) % W
-            run, c = _visible(j, r, causal)
-            if run:
-                o, lse = _merge(o, lse, *_pair_fwd(qs[r], ks[j], vs[j], c, scale))
+            plan = _plan(j, r, causal, zigzag)
+            if plan is None:
+                continue
+            q_, k_, c = plan
+            o_j, lse_j = _pair_fwd(_rows(qs[r], q_), _rows(ks[j], k_), _rows(vs[j], k_), c, scale)
+            if q_ == "all":
+                o, lse = _merge(o, lse, o_j, lse_j)
+            else:
+                o2, l2 = _merge(o[:, h:], lse[..., h:], o_j, lse_j)
+                o, lse = torch.cat([o[:, :h], o2], 1), torch.cat([lse[..., :h], l2], -1)
         outs.append(o.to(qs[r].dtype))
         lses.append(lse)
     if grad_outs is None:
@@ -231,14 +286,18 @@ def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_o
     dks = [torch.zeros(k.shape, dtype=torch.float32, device=k.device) for k in ks]
     dvs = [torch.zeros(v.shape, dtype=torch.float32, device=v.device) for v in vs]
     for r in range(W):
+        h = qs[r].shape[1] // 2
         for j in range(W):
-            run, c = _visible(j, r, causal)
-            if run:
-                dq, dk, dv = _pair_bwd(qs[r], ks[j], vs[j], outs[r], lses[r], grad_outs[r], c,
-                                       scale)
-                dqs[r] += dq
-                dks[j] += dk
-                dvs[j] += dv
+            plan = _plan(j, r, causal, zigzag)
+            if plan is None:
+                continue
+            q_, k_, c = plan
+            dq, dk, dv = _pair_bwd(_rows(qs[r], q_), _rows(ks[j], k_), _rows(vs[j], k_),
+                                   _rows(outs[r], q_), lses[r] if q_ == "all" else
+                                   lses[r][..., h:], _rows(grad_outs[r], q_), c, scale)
+            _rows(dqs[r], q_).add_(dq)
+            _rows(dks[j], k_).add_(dk)
+            _rows(dvs[j], k_).add_(dv)
     return outs, (dqs, dks, dvs)
 
 
@@ -246,7 +305,7 @@ def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_o
 # training integration
 # ---------------------------------------------------------------------------
 def get_batch_on_this_cp_rank(tensors, dim=1):
-    """This rank's contiguous chunk (along the sequence ``dim``) of every tensor."""
+    """This rank's zig-zag share (``zigzag_slice``) along the sequence ``dim``."""
     from . import state
     C = state.get_context_parallel_world_size()
     if C == 1:
@@ -257,8 +316,7 @@ def get_batch_on_this_cp_rank(tensors, dim=1):
         if t is None or not torch.is_tensor(t) or t.dim() <= dim:
             out.append(t)
             continue
-        c = t.shape[dim] // C
-        out.append(t.narrow(dim, r * c, c).contiguous())
+        out.append(zigzag_slice(t, dim, r, C).contiguous())
     return out
 
 
@@ -276,7 +334,9 @@ def cp_token_mean(losses, loss_mask):
 
 
 def chunk_position_ids(s, b, device):
-    """Global positions of this rank's chunk ``[b, s]``."""
+    """Global positions ``[b, s]`` of this rank's zig-zag share of ``s`` rows."""
     from . import state
+    C = state.get_context_parallel_world_size()
     r = state.get_context_parallel_rank()
-    return (r * s + torch.arange(s, device=device)).unsqueeze(0).expand(b, s)
+    full = torch.arange(s * C, device=device)
+    return zigzag_slice(full, 0, r, C).unsqueeze(0).expand(b, s)

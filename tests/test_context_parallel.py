@@ -16,52 +16,78 @@ def _full(b, s, nq, nkv, d, seed):
     return q, k, v, go
 
 
-def _ring_rank(rank, world, causal, nq, nkv):
+def _share(t, rank, world, zigzag):
+    from epfl_megatron_amd.parallel.context import zigzag_slice
+    if zigzag:
+        return zigzag_slice(t, 1, rank, world)
+    c = t.shape[1] // world
+    return t[:, rank * c:(rank + 1) * c]
+
+
+def _ring_rank(rank, world, causal, nq, nkv, zigzag):
     import torch.distributed as dist
     from epfl_megatron_amd.parallel.context import ring_attention
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b, s, d = 2, 12 * world, 16
     q, k, v, go = _full(b, s, nq, nkv, d, seed=3)
-    c = s // world
-    sl = slice(rank * c, (rank + 1) * c)
-    ql, kl, vl = (t[:, sl].clone().requires_grad_() for t in (q, k, v))
-    out = ring_attention(ql, kl, vl, dist.group.WORLD, causal=causal)
-    out.backward(go[:, sl])
+    ql, kl, vl = (_share(t, rank, world, zigzag).clone().requires_grad_() for t in (q, k, v))
+    out = ring_attention(ql, kl, vl, dist.group.WORLD, causal=causal, zigzag=zigzag)
+    out.backward(_share(go, rank, world, zigzag))
     return out.detach(), ql.grad, kl.grad, vl.grad
 
 
-@pytest.mark.parametrize("world,causal,nq,nkv", [(2, True, 4, 4), (4, True, 4, 2),
-                                                 (4, False, 4, 4), (2, False, 6, 2)])
-def test_ring_attention_matches_full(world, causal, nq, nkv):
+@pytest.mark.parametrize("world,causal,nq,nkv,zigzag", [
+    (2, True, 4, 4, False), (4, True, 4, 2, False), (4, False, 4, 4, False),
+    (2, False, 6, 2, False), (2, True, 4, 4, True), (4, True, 4, 2, True),
+    (3, True, 6, 2, True)])
+def test_ring_attention_matches_full(world, causal, nq, nkv, zigzag):
     from epfl_megatron_amd.ops.attention import attention_ref
-    res = run_dist(_ring_rank, world, causal, nq, nkv)
+    res = run_dist(_ring_rank, world, causal, nq, nkv, zigzag)
     b, s, d = 2, 12 * world, 16
     q, k, v, go = _full(b, s, nq, nkv, d, seed=3)
     qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
     ref = attention_ref(qr, kr, vr, causal=causal)
     ref.backward(go)
-    c = s // world
     for rank, (o, dq, dk, dv) in enumerate(res):
-        sl = slice(rank * c, (rank + 1) * c)
-        torch.testing.assert_close(o, ref.detach()[:, sl], atol=2e-5, rtol=2e-5)
-        torch.testing.assert_close(dq, qr.grad[:, sl], atol=5e-5, rtol=5e-5)
-        torch.testing.assert_close(dk, kr.grad[:, sl], atol=5e-5, rtol=5e-5)
-        torch.testing.assert_close(dv, vr.grad[:, sl], atol=5e-5, rtol=5e-5)
+        sh = lambda t: _share(t, rank, world, zigzag)  # noqa: E731
+        torch.testing.assert_close(o, sh(ref.detach()), atol=2e-5, rtol=2e-5)
+        torch.testing.assert_close(dq, sh(qr.grad), atol=5e-5, rtol=5e-5)
+        torch.testing.assert_close(dk, sh(kr.grad), atol=5e-5, rtol=5e-5)
+        torch.testing.assert_close(dv, sh(vr.grad), atol=5e-5, rtol=5e-5)
 
 
-def test_ring_attention_simulated_matches_full():
+def test_zigzag_plan_balances_causal_work():
+    """Every rank of a zig-zag ring does the same attention work (in units of
+    a quarter pair) at every W; the contiguous split does not."""
+    from epfl_megatron_amd.parallel.context import _plan
+    size = {"all": 2, "first": 1, "second": 1}
+    for W in (2, 4, 8):
+        def work(r, zz):
+            tot = 0
+            for j in range(W):
+                p = _plan(j, r, True, zz)
+                if p is not None:
+                    tot += size[p[0]] * size[p[1]] // (2 if p[2] else 1)
+            return tot
+        # quarter-pair units: diagonal (causal) 2, full pair 4, half pair 2
+        assert {work(r, True) for r in range(W)} == {2 * W}
+        assert work(0, False) == 2 and work(W - 1, False) == 4 * W - 2
+
+
+@pytest.mark.parametrize("zigzag", [False, True])
+def test_ring_attention_simulated_matches_full(zigzag):
     """The single-process ring (the GPU kernel test's form) on CPU."""
     from epfl_megatron_amd.ops.attention import attention_ref
     from epfl_megatron_amd.parallel.context import ring_attention_simulated
     W, b, s, nq, nkv, d = 3, 1, 24, 4, 2, 16
     q, k, v, go = _full(b, s, nq, nkv, d, seed=5)
-    c = s // W
-    ch = lambda t: [t[:, i * c:(i + 1) * c] for i in range(W)]  # noqa: E731
-    outs, (dqs, dks, dvs) = ring_attention_simulated(ch(q), ch(k), ch(v), True, grad_outs=ch(go))
+    ch = lambda t: [_share(t, i, W, zigzag) for i in range(W)]  # noqa: E731
+    outs, (dqs, dks, dvs) = ring_attention_simulated(ch(q), ch(k), ch(v), True, grad_outs=ch(go),
+                                                     zigzag=zigzag)
     qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
     ref = attention_ref(qr, kr, vr, causal=True)
     ref.backward(go)
-    torch.testing.assert_close(torch.cat(outs, 1), ref.detach(), atol=2e-5, rtol=2e-5)
-    torch.testing.assert_close(torch.cat(dqs, 1), qr.grad, atol=5e-5, rtol=5e-5)
-    torch.testing.assert_close(torch.cat(dks, 1), kr.grad, atol=5e-5, rtol=5e-5)
-    torch.testing.assert_close(torch.cat(dvs, 1), vr.grad, atol=5e-5, rtol=5e-5)
+    for got, want in ((outs, ref.detach()), (dqs, qr.grad), (dks, kr.grad), (dvs, vr.grad)):
+        for i in range(W):
+            torch.testing.assert_close(got[i].float(), _share(want, i, W, zigzag),
+                                       atol=5e-5, rtol=5e-5)

@@ -811,9 +811,10 @@ def test_deterministic_attention_backward_and_wgrad():
     assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])
 
 
-@pytest.mark.parametrize("W,causal,nq,nkv,hd", [(4, True, 8, 2, 128), (2, False, 4, 4, 64),
-                                                 (3, True, 6, 1, 128)])
-def test_ring_attention_kernels(W, causal, nq, nkv, hd):
+@pytest.mark.parametrize("W,causal,nq,nkv,hd,zigzag", [
+    (4, True, 8, 2, 128, False), (2, False, 4, 4, 64, False), (3, True, 6, 1, 128, False),
+    (4, True, 8, 2, 128, True), (2, True, 4, 4, 64, True)])
+def test_ring_attention_kernels(W, causal, nq, nkv, hd, zigzag):
     """Context-parallel ring attention (parallel/context.py) with the HIP
     FlashAttention kernels per (local Q, K/V chunk) pair: LSE merge in the
     forward, global-LSE pair backward; W ranks simulated in one process."""
@@ -826,15 +827,19 @@ def test_ring_attention_kernels(W, causal, nq, nkv, hd):
     k = torch.randn(b, s, nkv, hd, device=DEV, dtype=torch.bfloat16)
     v = torch.randn(b, s, nkv, hd, device=DEV, dtype=torch.bfloat16)
     go = torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16)
-    ch = lambda t: [t[:, i * c:(i + 1) * c].contiguous() for i in range(W)]  # noqa: E731
-    outs, (dqs, dks, dvs) = ring_attention_simulated(ch(q), ch(k), ch(v), causal, grad_outs=ch(go))
+    from epfl_megatron_amd.parallel.context import zigzag_slice
+    share = (lambda t, i: zigzag_slice(t, 1, i, W)) if zigzag else \
+        (lambda t, i: t[:, i * c:(i + 1) * c])  # noqa: E731
+    ch = lambda t: [share(t, i).contiguous() for i in range(W)]  # noqa: E731
+    outs, (dqs, dks, dvs) = ring_attention_simulated(ch(q), ch(k), ch(v), causal, grad_outs=ch(go),
+                                                     zigzag=zigzag)
     qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
     ref = attention_ref(qr, kr, vr, causal=causal)
     ref.backward(go.float())
-    _close(torch.cat(outs, 1), ref.detach(), 2e-2, 2e-2, "ring fwd")
-    _close(torch.cat(dqs, 1), qr.grad, 6e-2, 6e-2, "ring dq")
-    _close(torch.cat(dks, 1), kr.grad, 6e-2, 6e-2, "ring dk")
-    _close(torch.cat(dvs, 1), vr.grad, 6e-2, 6e-2, "ring dv")
+    for got, want, tol, name in ((outs, ref.detach(), 2e-2, "fwd"), (dqs, qr.grad, 6e-2, "dq"),
+                                 (dks, kr.grad, 6e-2, "dk"), (dvs, vr.grad, 6e-2, "dv")):
+        _close(torch.cat(got, 1), torch.cat([share(want, i) for i in range(W)], 1), tol, tol,
+               f"ring {name}")
 
 
 @pytest.mark.gpu
