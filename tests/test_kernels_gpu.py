@@ -864,3 +864,42 @@ def test_ring_pair_kernels_on_sequence_major_views():
                        causal, hd ** -0.5)
         for a, c in zip(g1, g2):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("F,kind", [(11008, 0), (5632, 1)])
+def test_decode_mlp_fused(M, F, kind):
+    """decode_mlp_k (csrc/skinny_gemm.hip): dense + residual, RMSNorm + fc1 +
+    GLU and fc2 + residual in one persistent launch with grid barriers equals
+    the three skinny launches bit for bit (same K split and summation order),
+    and the fp32 reference within bf16 tolerance; the barrier counter grows by
+    exactly 2 x grid per launch and records no timeout."""
+    C = _ext()
+    torch.manual_seed(M + F)
+    H, dt = 4096, torch.bfloat16
+    ctx = torch.randn(M, H, device=DEV, dtype=dt)
+    x = torch.randn(M, H, device=DEV, dtype=dt)
+    wo = (torch.randn(H, H, device=DEV) * H ** -0.5).to(dt)
+    w1 = (torch.randn(2 * F, H, device=DEV) * H ** -0.5).to(dt)
+    w2 = (torch.randn(H, F, device=DEV) * F ** -0.5).to(dt)
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).to(dt)
+    assert C.decode_mlp_supported(M, H, F)
+    sync = torch.zeros(2, dtype=torch.int64, device=DEV)
+    y = C.decode_mlp(ctx, x, wo, g, 1e-5, w1, w2, kind, sync)
+    y2 = C.decode_mlp(ctx, x, wo, g, 1e-5, w1, w2, kind, sync)
+    torch.cuda.synchronize()
+    grid = torch.cuda.get_device_properties(0).multi_processor_count
+    assert sync[1].item() == 0, "grid barrier timed out"
+    assert sync[0].item() == 4 * grid
+    h2 = C.skinny_norm_gemm(ctx, wo, None, 0.0, x)
+    a = C.skinny_norm_glu(h2, w1, g, 1e-5, kind)
+    ref3 = C.skinny_norm_gemm(a, w2, None, 0.0, h2)
+    assert torch.equal(y, ref3) and torch.equal(y2, ref3)
+    # fp32 reference
+    h2f = ctx.float() @ wo.float().t() + x.float()
+    hn = h2f * torch.rsqrt(h2f.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    u, v = (hn @ w1.float().t()).chunk(2, dim=-1)
+    act = {0: torch.nn.functional.silu, 1: torch.nn.functional.gelu}
+    af = u * act[kind](v)
+    yf = af @ w2.float().t() + h2f
+    _close(y, yf, 0.1, 3e-2, "decode_mlp vs fp32")
