@@ -18,9 +18,11 @@ forward   step i: chunk j = (r - i) mod W arrives from the previous rank.  For
 backward  with the GLOBAL O and LSE every (local Q, chunk j) pair yields its
           exact share of dQ, dK_j, dV_j from the FlashAttention backward
           (delta = rowsum(dO O) and P = exp(S - LSE) only need the global
-          values).  dQ stays local; (K_j, V_j, dK_j, dV_j) travel one hop per
-          step and after W hops every chunk is back at its owner with its
-          complete dK and dV.
+          values).  dQ stays local.  K/V travel as in the forward (posted
+          before the step's kernels); the dK_j / dV_j accumulators follow one
+          hop behind: posted after the step's kernels, received and added
+          after the NEXT step's kernels, so both transfers overlap compute.
+          After W hops every accumulator is back at its owner.
 
 The per-pair kernels are the training kernels (``csrc/flash_attn_fwd.hip`` /
 ``flash_attn_bwd.hip``: native GQA, LSE in natural log); on CPU tensors the
@@ -206,29 +208,40 @@ class _RingAttnFn(torch.autograd.Function):
         q, k, v, out, lse = ctx.saved_tensors
         ring = _Ring(ctx.group)
         W, r = ring.world, ring.rank
+        h = q.shape[1] // 2
         dout = dout.contiguous()
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
-        # the travelling chunk: K, V and its dK, dV accumulators (fp32)
-        buf = [k.contiguous(), v.contiguous(),
-               torch.zeros(k.shape, dtype=torch.float32, device=k.device),
-               torch.zeros(v.shape, dtype=torch.float32, device=v.device)]
+        kv = [k.contiguous(), v.contiguous()]
+        acc_work = acc_recv = None
         for i in range(W):
             j = (r - i) % W
+            kv_work = kv_recv = None
+            if i + 1 < W:  # K / V of the next step in flight during this one
+                kv_work, kv_recv = ring.shift(kv)
+            dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+            dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
             plan = _plan(j, r, ctx.causal, ctx.zigzag)
             if plan is not None:
                 qs, ks, c = plan
-                dq_j, dk_j, dv_j = _pair_bwd(_rows(q, qs), _rows(buf[0], ks), _rows(buf[1], ks),
-                                             _rows(out, qs), lse if qs == "all" else
-                                             lse[..., q.shape[1] // 2:],
+                dq_j, dk_j, dv_j = _pair_bwd(_rows(q, qs), _rows(kv[0], ks), _rows(kv[1], ks),
+                                             _rows(out, qs), lse if qs == "all" else lse[..., h:],
                                              _rows(dout, qs), c, ctx.scale)
                 _rows(dq, qs).add_(dq_j)
-                _rows(buf[2], ks).add_(dk_j)
-                _rows(buf[3], ks).add_(dv_j)
-            if W > 1:  # W hops bring every chunk back to its owner
-                work, recv = ring.shift(buf)
-                work.wait()
-                buf = recv
-        return (dq.to(q.dtype), buf[2].to(k.dtype), buf[3].to(v.dtype), None, None, None, None)
+                _rows(dk, ks).add_(dk_j)
+                _rows(dv, ks).add_(dv_j)
+            if acc_work is not None:  # chunk j's dK / dV so far, sent by the previous rank
+                acc_work.wait()
+                dk += acc_recv[0]
+                dv += acc_recv[1]
+            if W > 1:  # travels on while the next pair computes; W hops end at the owner
+                acc_work, acc_recv = ring.shift([dk, dv])
+            if kv_work is not None:
+                kv_work.wait()
+                kv = kv_recv
+        if acc_work is not None:
+            acc_work.wait()
+            dk, dv = acc_recv
+        return (dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None, None, None)
 
 
 def ring_attention(q, k, v, group, causal=True, softmax_scale=None, zigzag=False):
