@@ -32,7 +32,7 @@ from ..parallel import tensor as tp
 from ..ops.dropout import bias_dropout_add
 from ..utils.trace import trace_range, tracing
 from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync
-from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace
+from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace, rope_qkv
 from ..ops._ext import use_native, ext
 from ..parallel.context import chunk_position_ids, ring_attention
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
@@ -339,12 +339,14 @@ class ParallelAttention(MegatronModule):
         over the whole sequence: RoPE at the share's global positions, then the
         K/V ring (``parallel/context.py``) with the FlashAttention pair kernels."""
         sq, b = mixed.shape[:2]
-        q, k, v = self._split_qkv(mixed)
         if rope is not None:
             if position_ids is None:
                 position_ids = chunk_position_ids(sq, b, mixed.device)
-            q = apply_rope_ref(q, rope[0], rope[1], position_ids)
-            k = apply_rope_ref(k, rope[0], rope[1], position_ids)
+            g, r, hd = self.num_groups_per_partition, self.q_per_group, \
+                self.hidden_size_per_attention_head
+            mixed = rope_qkv(mixed.view(sq, b, g, r + 2, hd), rope[0], rope[1],
+                             position_ids.long()).view(sq, b, -1)
+        q, k, v = self._split_qkv(mixed)
         o = ring_attention(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1),
                            self.cp_group, causal=True, zigzag=True)
         return o.transpose(0, 1).reshape(sq, b, -1)

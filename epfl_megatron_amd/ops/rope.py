@@ -83,6 +83,27 @@ def rope_qkv_inplace(qkv5, cos, sin, position_ids=None, offset=0, inverse=False,
     return qkv5
 
 
+class _RopeQKVFn(torch.autograd.Function):
+    """Out-of-place rotation of the q and k heads of ``[s, b, ng, r+2, hd]``;
+    the backward rotates the gradient back (R^T), v passes through."""
+
+    @staticmethod
+    def forward(ctx, qkv5, cos, sin, position_ids):
+        ctx.save_for_backward(cos, sin, position_ids)
+        return rope_qkv_inplace(qkv5.contiguous().clone(), cos, sin, position_ids)
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin, position_ids = ctx.saved_tensors
+        return rope_qkv_inplace(g.contiguous().clone(), cos, sin, position_ids,
+                                inverse=True), None, None, None
+
+
+def rope_qkv(qkv5, cos, sin, position_ids):
+    """Autograd form of ``rope_qkv_inplace`` (HIP kernel on the GPU)."""
+    return _RopeQKVFn.apply(qkv5, cos, sin, position_ids)
+
+
 def apply_rotary_emb(xq, xk, cos, sin, position_ids=None, offset=0):
     """Out-of-place rotation of separate q ``[s,b,nq,d]`` and k ``[s,b,nk,d]``."""
     return (apply_rope_ref(xq, cos, sin, position_ids, offset),

@@ -903,3 +903,23 @@ def test_decode_mlp_fused(M, F, kind):
     af = u * act[kind](v)
     yf = af @ w2.float().t() + h2f
     _close(y, yf, 0.1, 3e-2, "decode_mlp vs fp32")
+
+
+def test_rope_qkv_autograd_matches_reference():
+    """ops/rope.py rope_qkv (the context-parallel path's RoPE: HIP kernel
+    forward, inverse rotation in the backward) vs apply_rope_ref autograd."""
+    from epfl_megatron_amd.ops.rope import apply_rope_ref, rope_qkv, rope_table
+    torch.manual_seed(4)
+    s, b, g, r, hd = 40, 2, 2, 3, 128
+    cos, sin = rope_table(hd, 256, DEV)
+    pos = torch.randint(0, 256, (b, s), device=DEV)
+    x = torch.randn(s, b, g, r + 2, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = rope_qkv(x, cos, sin, pos)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_()
+    qk = apply_rope_ref(xr[:, :, :, :r + 1].reshape(s, b, g * (r + 1), hd), cos, sin, pos)
+    yr = torch.cat([qk.view(s, b, g, r + 1, hd), xr[:, :, :, r + 1:]], 3)
+    yr.backward(gy.float())
+    _close(y, yr, 2e-2, 1e-2, "rope_qkv fwd")
+    _close(x.grad, xr.grad, 2e-2, 1e-2, "rope_qkv bwd")
