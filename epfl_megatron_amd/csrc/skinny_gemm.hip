@@ -64,7 +64,8 @@ __device__ __forceinline__ int64_t w_row(int blk, int r, int N) {
 // Output of one 16-feature block (t = the block's reduced fp32 tile; lane
 // holds column m = lane & 15, features 4 (lane >> 4) + i).
 template <typename T, int EPI, int ACT>
-__device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4& t, int lane) {
+__device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4& t, int lane,
+                                         int half = -1) {
   const int M = p.M;
   // D layout: lane holds column m = lane & 15, rows (features) 4 (lane >> 4) + i
   const int m = lane & 15, nr = 4 * (lane >> 4);
@@ -77,11 +78,14 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
     typename fa::MT<T>::x4 gt;
 #pragma unroll
     for (int i = 0; i < 4; ++i) gt[i] = (T)__shfl_xor((float)o[i], 32, 64);
-    if (lane < 32 && m < M) {
+    // half block (half >= 0): features 4 half .. 4 half + 3 only, in MFMA
+    // rows 0-3 / 8-11 (rows 4-7 / 12-15 duplicate them and are not stored)
+    if ((half < 0 ? lane < 32 : lane < 16) && m < M) {
       typename fa::MT<T>::x4 out;
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[i] = (T)((float)o[i] * act<ACT>((float)gt[i]));
-      *reinterpret_cast<typename fa::MT<T>::x4*>(y + (int64_t)m * p.ldy + blk * 8 + nr) = out;
+      const int f = blk * 8 + (half < 0 ? nr : 4 * half);
+      *reinterpret_cast<typename fa::MT<T>::x4*>(y + (int64_t)m * p.ldy + f) = out;
     }
     return;
   }
@@ -280,11 +284,29 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   const int r = lane & 15, kc = 8 * (lane >> 4);
   const bool xon = r < M;
   const int nblocks = EPI == EPI_GLU ? N / 8 : N / 16;
-  const int G = (int)gridDim.x;
-  auto wptr = [&](int blk) { return w + w_row<EPI>(blk, r, N) * K + kbeg + kc; };
-  int blk = blockIdx.x;
-  const T* wr = wptr(blk);
-  const T* wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
+  const int G = (int)gridDim.x, wg = blockIdx.x;
+  // Work units of this workgroup: blocks wg, wg + G, ...  GLU tail: when the
+  // last round has nrem <= G / 2 blocks, they run as 2 nrem HALF blocks (4
+  // features each) on 2 nrem workgroups instead of nrem full ones: the
+  // round's time halves (Llama-2-7B fc1: 1376 blocks = 5 x 256 + 96 ->
+  // at most 5.5 instead of 6 block times per workgroup).  A half block's MFMA
+  // rows r and r + 4 read the same W row (one HBM fetch per cache line).
+  const int nrem = nblocks % G;
+  const bool halves = EPI == EPI_GLU && nrem > 0 && 2 * nrem <= G;
+  const int rounds = halves ? (nblocks - nrem) / G : 0;
+  const int nunits = halves ? rounds + (wg < 2 * nrem ? 1 : 0) : (nblocks - wg + G - 1) / G;
+  auto unit_blk = [&](int j) { return j < rounds || !halves ? wg + j * G : nblocks - nrem + wg / 2; };
+  auto unit_half = [&](int j) { return j < rounds || !halves ? -1 : (wg & 1); };
+  auto wptr = [&](int j) {
+    const int b = unit_blk(j), h = unit_half(j);
+    int64_t row;
+    if (h < 0) row = w_row<EPI>(b, r, N);
+    else row = (r < 8 ? 0 : (int64_t)N) + (int64_t)b * 8 + 4 * h + (r & 3);
+    return w + row * K + kbeg + kc;
+  };
+  int j = 0, blk = unit_blk(0), half = unit_half(0);
+  const T* wr = wptr(0);
+  const T* wn = wptr(nunits > 1 ? 1 : 0);
 
   x8 a[U];
 #pragma unroll
@@ -355,8 +377,8 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
     }
     return acc;
   };
-  for (int j = 0;; ++j) {
-    const bool last = blk + G >= nblocks;
+  for (;; ++j) {
+    const bool last = j + 1 >= nunits;
     const f4 acc = last ? run_block(std::true_type{}) : run_block(std::false_type{});
     part[j & 1][wave][lane] = acc;
     __syncthreads();
@@ -364,12 +386,13 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
       f4 t = part[j & 1][0][lane];
 #pragma unroll
       for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][lane];  // fixed order
-      epilogue<T, EPI, ACT>(p, blk, t, lane);
+      epilogue<T, EPI, ACT>(p, blk, t, lane, half);
     }
     if (last) break;
-    blk += G;
+    blk = unit_blk(j + 1);
+    half = unit_half(j + 1);
     wr = wn;
-    wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
+    wn = wptr(j + 2 < nunits ? j + 2 : nunits - 1);
   }
 }
 

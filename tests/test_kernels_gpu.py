@@ -512,10 +512,13 @@ def test_skinny_fused_norm_residual(M, N, K):
 
 
 @pytest.mark.parametrize("kind,name", [(0, "swiglu"), (1, "geglu")])
-@pytest.mark.parametrize("M,F,K", [(1, 11008, 4096), (8, 512, 512), (16, 1376, 4096)])
+@pytest.mark.parametrize("M,F,K", [(1, 11008, 4096), (8, 512, 512), (16, 1376, 4096),
+                                   (3, 2816, 4096), (5, 5632, 4096)])
 def test_skinny_fused_glu(M, F, K, kind, name):
     """fc1 decode projection with the norm prologue and the GLU epilogue vs
-    rmsnorm -> skinny GEMM -> glu kernel."""
+    rmsnorm -> skinny GEMM -> glu kernel.  F = 11008 / 2816 on 256 CUs run
+    the last round as half blocks (1376 = 5 x 256 + 96, 352 = 256 + 96);
+    5632 (704 = 2 x 256 + 192) keeps full blocks."""
     from epfl_megatron_amd.ops.norms import rms_norm
     from epfl_megatron_amd.ops.activations import glu
     C = _ext()
