@@ -27,6 +27,7 @@ Other BASELINE configs, one command each (need >= tp*pp GPUs):
     --preset llama7b-tp8-seq4096     Llama-2-7B, TP=8 (SP), seq 4096
     --preset falcon40b-tp4-pp2       Falcon-40B, TP=4 x PP=2 interleaved, 8 micro-batches
     --preset llama70b-tp8            Llama-2-70B, TP=8 (SP), full recompute, dist-opt
+    --preset llama7b-cp8-seq32k      Llama-2-7B, seq 32768 split over 8 GPUs (context parallel)
 1-GPU per-rank proxies of the TP configs (TP rank 0 of the real model built by
 --simulated_tensor_parallel_size: per-rank GEMM / attention shapes, s/tp-row
 norms and residuals under SP, TP collectives looped back locally and reported
@@ -71,6 +72,10 @@ PRESETS = {
     # of the activations: the memory model picks the recompute depth)
     "llama70b-tp8": dict(model="llama2-70b", tp=8, pp=1, seq=4096, mbs=2, nmicro=8, sp=True,
                          recompute_budget_gb=260, dist_opt=True),
+    # MI355X addition (no reference counterpart): long-context training with
+    # context parallelism, each 32k-token sequence split over 8 GPUs (zig-zag
+    # ring attention, parallel/context.py)
+    "llama7b-cp8-seq32k": dict(model="llama2-7b", tp=1, pp=1, cp=8, seq=32768, mbs=1, nmicro=8),
 }
 
 PROXIES = {  # one TP rank of a BASELINE config on one GPU
@@ -93,6 +98,7 @@ def _parse(argv=None):
     ap.add_argument("--num_micro", type=int, default=None, help="micro-batches per step")
     ap.add_argument("--tp", type=int, default=None)
     ap.add_argument("--pp", type=int, default=None)
+    ap.add_argument("--cp", type=int, default=None, help="context-parallel size")
     ap.add_argument("--vpp_layers", type=int, default=None,
                     help="layers per virtual pipeline stage (interleaved 1F1B)")
     ap.add_argument("--recompute", default=None, choices=["selective", "full"])
@@ -152,7 +158,7 @@ def _resolve(a, world):
         cfg = dict(PRESETS[PROXIES[a.proxy][0]])
         proxy_tp = PROXIES[a.proxy][1]
     for k, v in (("model", a.model), ("seq", a.seq_len), ("mbs", a.micro_batch),
-                 ("nmicro", a.num_micro), ("tp", a.tp), ("pp", a.pp),
+                 ("nmicro", a.num_micro), ("tp", a.tp), ("pp", a.pp), ("cp", a.cp),
                  ("vpp_layers", a.vpp_layers), ("recompute", a.recompute),
                  ("recompute_budget_gb", a.recompute_budget_gb)):
         if v is not None:
@@ -171,10 +177,10 @@ def _resolve(a, world):
 
 
 def _framework_argv(a, cfg, shape, world, on_gpu):
-    tp, pp = cfg.get("tp", 1), cfg.get("pp", 1)
-    if world % (tp * pp):
-        raise SystemExit(f"--gpus {world} is not a multiple of tp*pp = {tp * pp}")
-    dp = world // (tp * pp)
+    tp, pp, cp = cfg.get("tp", 1), cfg.get("pp", 1), cfg.get("cp", 1) or 1
+    if world % (tp * pp * cp):
+        raise SystemExit(f"--gpus {world} is not a multiple of tp*pp*cp = {tp * pp * cp}")
+    dp = world // (tp * pp * cp)  # ranks reading different samples
     mbs, nmicro, seq = cfg["mbs"], cfg["nmicro"], cfg["seq"]
     gbs = mbs * nmicro * dp
     s = shape
@@ -192,7 +198,8 @@ def _framework_argv(a, cfg, shape, world, on_gpu):
             "NullTokenizer", "--synthetic_data", "--synthetic_pattern", a.data,
             "--synthetic_vocab_size", str(s["vocab"]), "--make_vocab_size_divisible_by", "128",
             "--num_workers", "0", "--ddp_bucket_size_mb", str(a.bucket_mb),
-            "--tensor_model_parallel_size", str(tp), "--pipeline_model_parallel_size", str(pp)]
+            "--tensor_model_parallel_size", str(tp), "--pipeline_model_parallel_size", str(pp),
+            "--context_parallel_size", str(cp)]
     if s.get("ffn"):
         argv += ["--ffn_hidden_size", str(s["ffn"])]
     if s.get("nkv"):
@@ -219,7 +226,7 @@ def _framework_argv(a, cfg, shape, world, on_gpu):
         argv += ["--bf16"]
     else:
         argv += ["--distributed_backend", "gloo"]
-    dist_opt = (dp > 1 or cfg.get("dist_opt")) and not a.no_dist_opt
+    dist_opt = (dp * cp > 1 or cfg.get("dist_opt")) and not a.no_dist_opt
     if dist_opt:
         argv += ["--use_distributed_optimizer"]
     rc = cfg.get("recompute")
@@ -232,7 +239,7 @@ def _framework_argv(a, cfg, shape, world, on_gpu):
         argv += ["--recompute_memory_budget_gb", str(cfg["recompute_budget_gb"])]
     if a.extra:
         argv += a.extra.split()
-    return argv, dict(tp=tp, pp=pp, dp=dp, gbs=gbs, mbs=mbs, nmicro=nmicro, seq=seq,
+    return argv, dict(tp=tp, pp=pp, cp=cp, dp=dp, gbs=gbs, mbs=mbs, nmicro=nmicro, seq=seq,
                       dist_opt=bool(dist_opt), vpp=cfg.get("vpp_layers") if pp > 1 else None,
                       recompute=rc, sp=bool(cfg.get("sp") and (tp > 1 or sim_tp)),
                       sim_tp=sim_tp)
@@ -379,6 +386,8 @@ def main(argv=None):
         if par["tp"] > 1:
             parallel = f"tp{par['tp']}" + ("+sp" if par["sp"] else "") + \
                 (f"_dp{par['dp']}" if par["dp"] > 1 else "")
+        if par["cp"] > 1:
+            parallel += f"+cp{par['cp']}"
         if par["pp"] > 1:
             parallel += f"_pp{par['pp']}" + (f"+vpp{par['vpp']}" if par["vpp"] else "")
         if par["dist_opt"]:
@@ -427,7 +436,7 @@ def main(argv=None):
             "max_mem_gb": round(float(mem[0]), 1) if on_gpu else None,
             "backend": dist.get_backend(),
             "world_size": world,
-            "dp": par["dp"], "tp": par["tp"], "pp": par["pp"],
+            "dp": par["dp"], "tp": par["tp"], "pp": par["pp"], "cp": par["cp"],
             "recompute": {"granularity": args.recompute_granularity,
                           "method": args.recompute_method,
                           "layers": (args.recompute_num_layers

@@ -103,3 +103,14 @@ def test_proxy_is_one_simulated_tp_rank():
     assert coll["all_gather"]["calls_per_step"] > 0 and coll["reduce_scatter"]["calls_per_step"] > 0
     assert rec["proxy_tp_comm_ms_per_step_analytic"] > 0
     assert rec["tokens_per_sec_per_gpu"] * 8 == pytest.approx(rec["value"], rel=1e-3)
+
+
+def test_bench_context_parallel_preset_on_gloo():
+    """--preset llama7b-cp8-seq32k scaled down (tiny model, seq 256, CP=2 at 4
+    ranks): 2 sample-parallel ranks x 2 sequence chunks, dist-opt over all 4."""
+    rec = _run(["--gpus", "4", "--preset", "llama7b-cp8-seq32k", "--cp", "2", "--model", "tiny",
+                "--seq_len", "256", "--num_micro", "2", "--steps", "1", "--warmup", "1"])
+    assert rec["config"]["parallelism"] == "dp2+cp2+distopt"
+    assert (rec["dp"], rec["cp"]) == (2, 2)
+    assert rec["config"]["global_batch"] == 2 * 2 * rec["config"]["micro_batch"]
+    assert rec["value"] > 0 and rec["final_loss"] == rec["final_loss"]
