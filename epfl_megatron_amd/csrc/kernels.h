@@ -246,6 +246,7 @@ struct SkinnyArgs {
   int64_t c_ss, c_sb;
   const int64_t* slot_ptr;  // device slot index (graph decode) or nullptr: `slot`
   int64_t slot;
+  int no_halves;        // 1: the persistent GLU keeps full blocks in its last round (A/B)
 };
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
 // one persistent launch for a decode layer's MLP side (TP = 1): pa = dense +

@@ -292,7 +292,7 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   // at most 5.5 instead of 6 block times per workgroup).  A half block's MFMA
   // rows r and r + 4 read the same W row (one HBM fetch per cache line).
   const int nrem = nblocks % G;
-  const bool halves = EPI == EPI_GLU && nrem > 0 && 2 * nrem <= G;
+  const bool halves = EPI == EPI_GLU && nrem > 0 && 2 * nrem <= G && !p.no_halves;
   const int rounds = halves ? (nblocks - nrem) / G : 0;
   const int nunits = halves ? rounds + (wg < 2 * nrem ? 1 : 0) : (nblocks - wg + G - 1) / G;
   auto unit_blk = [&](int j) { return j < rounds || !halves ? wg + j * G : nblocks - nrem + wg / 2; };
@@ -771,7 +771,14 @@ bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
 // CU) latency-bound at ~3.2 TB/s.  EMA_SKINNY_WAVES=4 forces the 4-wave form.
 // K = 4096 / 8192 (16 / 32 k-steps per wave) take the persistent form
 // (EMA_SKINNY_PERSIST=0: the one-block-per-workgroup kernel everywhere).
-void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s) {
+void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
+  // EMA_SKINNY_HALVES=0: no half-block last round for the GLU (A/B)
+  static const int no_halves = [] {
+    const char* e = getenv("EMA_SKINNY_HALVES");
+    return e && e[0] == '0' ? 1 : 0;
+  }();
+  SkinnyArgs p = p0;
+  p.no_halves = no_halves;
   static const int want = [] {
     const char* e = getenv("EMA_SKINNY_WAVES");
     return e ? atoi(e) : 8;
