@@ -27,7 +27,9 @@ Other BASELINE configs, one command each (need >= tp*pp GPUs):
     --preset llama7b-tp8-seq4096     Llama-2-7B, TP=8 (SP), seq 4096
     --preset falcon40b-tp4-pp2       Falcon-40B, TP=4 x PP=2 interleaved, 8 micro-batches
     --preset llama70b-tp8            Llama-2-70B, TP=8 (SP), full recompute, dist-opt
-    --preset llama7b-cp8-seq32k      Llama-2-7B, seq 32768 split over 8 GPUs (context parallel)
+    --preset llama70b-tp8-budget     the same with the memory-model recompute policy (260 GB)
+    --preset llama7b-cp8-seq32k      Llama-2-7B, seq 32768 split over 8 GPUs (context parallel;
+                                     ring verified on gloo and on one GPU, not yet over RCCL)
 1-GPU per-rank proxies of the TP configs (TP rank 0 of the real model built by
 --simulated_tensor_parallel_size: per-rank GEMM / attention shapes, s/tp-row
 norms and residuals under SP, TP collectives looped back locally and reported
@@ -67,11 +69,13 @@ PRESETS = {
     # config #4
     "falcon40b-tp4-pp2": dict(model="falcon-40b", tp=4, pp=2, vpp_layers=10, seq=2048, mbs=2,
                               nmicro=8, sp=True),
-    # config #5
-    # (the reference recomputes every layer; 288 GB per MI355X holds most or all
-    # of the activations: the memory model picks the recompute depth)
+    # config #5 as the reference runs it: every layer recomputed
     "llama70b-tp8": dict(model="llama2-70b", tp=8, pp=1, seq=4096, mbs=2, nmicro=8, sp=True,
-                         recompute_budget_gb=260, dist_opt=True),
+                         recompute="full", dist_opt=True),
+    # MI355X variant of config #5: 288 GB per GPU holds most or all of the
+    # activations, so the memory model picks the recompute depth for a 260 GB peak
+    "llama70b-tp8-budget": dict(model="llama2-70b", tp=8, pp=1, seq=4096, mbs=2, nmicro=8,
+                                sp=True, recompute_budget_gb=260, dist_opt=True),
     # MI355X addition (no reference counterpart): long-context training with
     # context parallelism, each 32k-token sequence split over 8 GPUs (zig-zag
     # ring attention, parallel/context.py)
@@ -81,6 +85,7 @@ PRESETS = {
 PROXIES = {  # one TP rank of a BASELINE config on one GPU
     "llama7b-tp8": ("llama7b-tp8-seq4096", 8),
     "llama70b-tp8": ("llama70b-tp8", 8),
+    "llama70b-tp8-budget": ("llama70b-tp8-budget", 8),
     "falcon40b-tp4-pp2": ("falcon40b-tp4-pp2", 4),
 }
 

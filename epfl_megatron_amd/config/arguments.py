@@ -570,6 +570,11 @@ def _derive_recompute_and_parallel_features(args):
         _require(not args.reset_attention_mask,
                  "--reset_attention_mask is not supported with context parallelism")
         _require(not sim_tp, "--simulated_tensor_parallel_size excludes context parallelism")
+        # the ring-attention pair kernels apply no attention dropout:
+        # refuse a configuration whose CP=1 counterpart would drop attention probs
+        _require(args.attention_dropout == 0 or args.use_flash_attn,
+                 "context parallelism applies no attention dropout: set --attention_dropout 0 "
+                 "(or --use_flash_attn, which has none either)")
     # Reference defect D17: the GQA view silently breaks when KV heads do not
     # split evenly over TP ranks; we check it explicitly.
     if args.num_attention_heads_kv % (sim_tp or args.tensor_model_parallel_size) != 0:

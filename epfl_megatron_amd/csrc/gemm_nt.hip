@@ -52,6 +52,7 @@
 // written to, a strided set of row groups of a larger matrix — one chunk of
 // the sequence-parallel all-gather / reduce-scatter pipeline
 // (parallel/tensor/layers.py) runs as one launch without a copy.
+#include <algorithm>
 #include <cstdlib>
 
 #include "act_math.h"
@@ -554,6 +555,353 @@ __global__ void __launch_bounds__(256, 1) gemm_nt4_k(NtArgs p) {
                                   n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
 }
 
+// ---- 4-wave variant, early-refill schedule (variant 5) ---------------------
+// Same tile, LDS image and fragment sets as gemm_nt4_k, but each operand's
+// half of a ring slot is refilled as soon as every wave has read it, and the
+// wait for the next K-step sits three quarters into the current one, so a
+// DMA piece has 1.0-1.5 K-steps (not 0.5-1.0) to land.  One K-step = 32
+// groups of 4 MFMAs; after group G:
+//   G 0-3   read 2 A fragments of (t, k-half 1) -> set1
+//   G 5     lgkmcnt(0), BARRIER 1   (A of slot t read by every wave)
+//   G 6-13  DMA one A piece of step t+2 -> slot t
+//   G 6-9   read 2 B fragments of (t, k-half 1) -> set1
+//   G 11    lgkmcnt(0), BARRIER 2   (B of slot t read by every wave)
+//   G 12-19 DMA one B piece of step t+2 -> slot t
+//   G 23    vmcnt(16), BARRIER 3    (step t+1 landed, own DMA then everyone's)
+//   G 24-31 read 2 fragments of (t+1, k-half 0) -> set0 from slot t+1
+// then lgkmcnt(0).  Groups 0-15 run on set0 (k-half 0), 16-31 on set1.
+template <typename T, int EPI, int ACT>
+__global__ void __launch_bounds__(256, 1) gemm_nt5_k(NtArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
+  typedef typename fa::MT<T>::x8 X8;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntiles = p.ntm * p.ntn;
+  const int lin = xcd_remap((int)blockIdx.x, ntiles);
+  const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
+  const int64_t m0 = (int64_t)tt.x * TM;
+  const int64_t n0 = (int64_t)tt.y * (EPI == EPI_GLU ? TN / 2 : TN);
+  const int M = p.M, N = p.N;
+
+  uint32_t off[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = 8 * (8 * wave + i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((tr >> 1) & 7);
+    int64_t am = m0 + tr;
+    am = map_row(am < M ? am : M - 1, p.am);
+    off[i] = (uint32_t)((am * p.lda + 8 * c) * (int64_t)sizeof(T));
+    int64_t bn;
+    if constexpr (EPI == EPI_GLU) {
+      const int band = tr >> 7, q = tr & 127;
+      const int64_t f = n0 + 64 * band + (q & 63);
+      bn = f < N ? (q < 64 ? f : N + f) : 0;
+    } else {
+      bn = n0 + tr;
+      bn = bn < N ? bn : N - 1;
+    }
+    off[8 + i] = (uint32_t)((bn * p.ldb + 8 * c) * (int64_t)sizeof(T));
+  }
+  const char* const abyte = reinterpret_cast<const char*>(p.a);
+  const char* const bbyte = reinterpret_cast<const char*>(p.b);
+  char* const ldsp = lds;
+  const int nt = p.K / BK2;
+  auto stage_piece = [&](int q, int ts, int slot) {
+    const char* base = (q < 8 ? abyte : bbyte) + (int64_t)ts * (BK2 * (int)sizeof(T));
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(base + off[q]),
+                                     (__attribute__((address_space(3))) void*)(ldsp + dst), 16, 0, 0);
+  };
+
+  f32x4 acc[8][8];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  const int fr = lane & 15, fsw = (fr >> 1) & 7;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const uint32_t ch = 16u * (uint32_t)(((lane >> 4) + 4 * kh) ^ fsw);
+    abase[kh] = lds_base + 128u * (128u * wm + fr) + ch;
+    bbase[kh] = lds_base + OPB2 + 128u * (128u * wn + fr) + ch;
+  }
+  X8 set0[16], set1[16];
+  auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
+    constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
+    if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
+    else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto mfma4 = [&](X8 (&cur)[16], auto g) {
+    constexpr int G = decltype(g)::value;
+    static_for<4>([&](auto q) {
+      constexpr int IDX = 4 * G + decltype(q)::value, I = IDX / 8, J = IDX % 8;
+      mfma_acc<T>(acc[I][J], cur[8 + J], cur[I]);
+    });
+  };
+
+  static_for<16>([&](auto q) { stage_piece(decltype(q)::value, 0, 0); });
+  static_for<16>([&](auto q) { stage_piece(decltype(q)::value, min(1, nt - 1), 1); });
+  {
+    X8 z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = (T)0.f;
+    static_for<64>([&](auto q) {
+      constexpr int I = decltype(q)::value / 8, J = decltype(q)::value % 8;
+      mfma_zero<T>(acc[I][J], z);
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  static_for<16>([&](auto f) { read_frag(set0, f, K0{}, 0u); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int t = 0; t < nt; ++t) {
+    const uint32_t so = (uint32_t)((t & 1) * SLOTB2), sn = (uint32_t)(SLOTB2 - so);
+    const int ts = min(t + 2, nt - 1), slot = t & 1;
+    static_for<32>([&](auto g) {
+      constexpr int G = decltype(g)::value;
+      if constexpr (G < 16) mfma4(set0, std::integral_constant<int, G>{});
+      else mfma4(set1, std::integral_constant<int, G - 16>{});
+      if constexpr (G < 4) {
+        read_frag(set1, std::integral_constant<int, 2 * G>{}, K1{}, so);
+        read_frag(set1, std::integral_constant<int, 2 * G + 1>{}, K1{}, so);
+      }
+      if constexpr (G == 5 || G == 11) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+      }
+      if constexpr (G >= 6 && G < 14) stage_piece(G - 6, ts, slot);
+      if constexpr (G >= 6 && G < 10) {
+        read_frag(set1, std::integral_constant<int, 8 + 2 * (G - 6)>{}, K1{}, so);
+        read_frag(set1, std::integral_constant<int, 9 + 2 * (G - 6)>{}, K1{}, so);
+      }
+      if constexpr (G >= 12 && G < 20) stage_piece(8 + G - 12, ts, slot);
+      if constexpr (G == 23) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+      }
+      if constexpr (G >= 24) {
+        read_frag(set0, std::integral_constant<int, 2 * (G - 24)>{}, K0{}, sn);
+        read_frag(set0, std::integral_constant<int, 2 * (G - 24) + 1>{}, K0{}, sn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  fa::mfma_drain();
+
+  char* reg = lds + wave * 32768;
+  acc_to_lds<T, 8>(acc, reg, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  epilogue_rows<T, EPI, ACT, 128>(p, reg, lane, m0 + 128 * wm,
+                                  n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
+}
+
+// ---- persistent 4-wave variant (variant 6, EPI_STORE without row maps) ------
+// The early-refill K-step of gemm_nt5_k, run as one continuous stream of
+// K-steps over all the tiles a workgroup owns (grid = one workgroup per CU,
+// tiles dealt round-robin in XCD-grouped order).  The DMA of the next tile's
+// first two K-steps rides in the current tile's last two K-steps, so a tile
+// starts with its operands already in LDS; the epilogue goes from registers
+// straight to global memory (bf16 pack + two permlane swaps give each lane 8
+// consecutive columns, one 16-B store per fragment pair), leaving the LDS ring
+// to the next tile's data; the first k-half of a tile accumulates onto C = 0.
+// Operands are read by buffer_load ... lds through a per-tile descriptor whose
+// size ends at the last valid row: rows past M / N read as zeros (no clamping).
+template <typename T>
+__device__ __forceinline__ void mfma_acc0(f32x4& acc, typename fa::MT<T>::x8 a,
+                                          typename fa::MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16))
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+
+template <typename T>
+__device__ __forceinline__ uint2 pack4(f32x4 v) {
+  typename fa::MT<T>::x4 h;
+  h[0] = (T)v[0]; h[1] = (T)v[1]; h[2] = (T)v[2]; h[3] = (T)v[3];
+  return *reinterpret_cast<uint2*>(&h);
+}
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+template <typename T, int EPI, int ACT>
+__global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
+  typedef typename fa::MT<T>::x8 X8;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = p.ntm * p.ntn;
+  const int G = gridDim.x, bid = blockIdx.x;
+  if (bid >= ntiles) return;
+  const int nmine = (ntiles - 1 - bid) / G + 1;
+  const int M = p.M, N = p.N;
+  const int nt = p.K / BK2;  // >= 2 (host-checked)
+
+  // per-lane DMA byte offsets inside a tile (fixed for the whole kernel)
+  uint32_t off[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = 8 * (8 * wave + i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((tr >> 1) & 7);
+    off[i] = (uint32_t)(tr * p.lda + 8 * c) * (uint32_t)sizeof(T);
+    off[8 + i] = (uint32_t)(tr * p.ldb + 8 * c) * (uint32_t)sizeof(T);
+  }
+  // tile i of this workgroup -> (m0, n0)
+  auto tile_org = [&](int i, int64_t& m0, int64_t& n0) {
+    const int base = i * G, rem = min(G, ntiles - base);
+    const int lin = base + xcd_remap(bid, rem);
+    const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
+    m0 = (int64_t)tt.x * TM;
+    n0 = (int64_t)tt.y * TN;
+  };
+  // descriptors of tile i (size 0 past the last tile: every load is dropped)
+  auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
+    int64_t m0 = 0, n0 = 0;
+    int64_t na = 0, nb = 0;
+    if (i < nmine) {
+      tile_org(i, m0, n0);
+      na = (int64_t)(M - m0) * p.lda * (int64_t)sizeof(T);
+      nb = (int64_t)(N - n0) * p.ldb * (int64_t)sizeof(T);
+    }
+    const char* a = reinterpret_cast<const char*>(p.a) + m0 * p.lda * (int64_t)sizeof(T);
+    const char* b = reinterpret_cast<const char*>(p.b) + n0 * p.ldb * (int64_t)sizeof(T);
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, (int)min(na, (int64_t)0x7fffffff), 0x00020000);
+    rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)min(nb, (int64_t)0x7fffffff), 0x00020000);
+  };
+  char* const ldsp = lds;
+  auto dma = [&](int q, Rsrc r, uint32_t soff, int slot) {
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
+                                             16, off[q], soff, 0, 0);
+  };
+
+  f32x4 acc[8][8];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  const int fr = lane & 15, fsw = (fr >> 1) & 7;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const uint32_t ch = 16u * (uint32_t)(((lane >> 4) + 4 * kh) ^ fsw);
+    abase[kh] = lds_base + 128u * (128u * wm + fr) + ch;
+    bbase[kh] = lds_base + OPB2 + 128u * (128u * wn + fr) + ch;
+  }
+  X8 set0[16], set1[16];
+  auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
+    constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
+    if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
+    else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto mfma4 = [&](X8 (&cur)[16], auto g, auto zero) {
+    constexpr int GG = decltype(g)::value;
+    static_for<4>([&](auto q) {
+      constexpr int IDX = 4 * GG + decltype(q)::value, I = IDX / 8, J = IDX % 8;
+      if constexpr (decltype(zero)::value) mfma_acc0<T>(acc[I][J], cur[8 + J], cur[I]);
+      else mfma_acc<T>(acc[I][J], cur[8 + J], cur[I]);
+    });
+  };
+
+  Rsrc ra_c, rb_c, ra_n, rb_n;  // current / next tile
+  make_rsrc(0, ra_c, rb_c);
+  make_rsrc(1, ra_n, rb_n);
+  static_for<8>([&](auto q) { dma(decltype(q)::value, ra_c, 0u, 0); });
+  static_for<8>([&](auto q) { dma(8 + decltype(q)::value, rb_c, 0u, 0); });
+  static_for<8>([&](auto q) { dma(decltype(q)::value, ra_c, BK2 * sizeof(T), 1); });
+  static_for<8>([&](auto q) { dma(8 + decltype(q)::value, rb_c, BK2 * sizeof(T), 1); });
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  static_for<16>([&](auto f) { read_frag(set0, f, K0{}, 0u); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  int par = 0;  // LDS slot of K-step 0 of the current tile
+  for (int i = 0; i < nmine; ++i) {
+    auto kstep = [&](int t, auto zero) {
+      const int slot = (t + par) & 1;
+      const uint32_t so = (uint32_t)(slot * SLOTB2), sn = (uint32_t)(SLOTB2 - so);
+      // source of K-step t+2: this tile, else the next tile's step t+2-nt
+      const bool here = t + 2 < nt;
+      const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
+      const uint32_t soff = (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
+      static_for<32>([&](auto g) {
+        constexpr int GG = decltype(g)::value;
+        if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
+        else mfma4(set1, std::integral_constant<int, GG - 16>{}, std::false_type{});
+        if constexpr (GG < 4) {
+          read_frag(set1, std::integral_constant<int, 2 * GG>{}, K1{}, so);
+          read_frag(set1, std::integral_constant<int, 2 * GG + 1>{}, K1{}, so);
+        }
+        if constexpr (GG == 5 || GG == 11) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (GG >= 6 && GG < 14) dma(GG - 6, ra, soff, slot);
+        if constexpr (GG >= 6 && GG < 10) {
+          read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
+          read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
+        }
+        if constexpr (GG >= 12 && GG < 20) dma(8 + GG - 12, rb, soff, slot);
+        if constexpr (GG == 23) {
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (GG >= 24) {
+          read_frag(set0, std::integral_constant<int, 2 * (GG - 24)>{}, K0{}, sn);
+          read_frag(set0, std::integral_constant<int, 2 * (GG - 24) + 1>{}, K0{}, sn);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    kstep(0, std::true_type{});
+    for (int t = 1; t < nt; ++t) kstep(t, std::false_type{});
+
+    // epilogue of tile i: registers -> global, while the next tile's first two
+    // K-steps are (or have been) landing in LDS
+    fa::mfma_drain();
+    int64_t m0, n0;
+    tile_org(i, m0, n0);
+    T* c = reinterpret_cast<T*>(p.c);
+    const int q = lane >> 4;
+    const int64_t col0 = n0 + 128 * wn + 8 * q;
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+      const int64_t row = m0 + 128 * wm + 16 * ii + (lane & 15);
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        uint2 x = pack4<T>(acc[ii][2 * jp]), y = pack4<T>(acc[ii][2 * jp + 1]);
+        auto s0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+        auto s1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+        auto t0 = __builtin_amdgcn_permlane16_swap(s0[0], s0[1], false, false);
+        auto t1 = __builtin_amdgcn_permlane16_swap(s1[0], s1[1], false, false);
+        const int64_t col = col0 + 32 * jp;
+        if (row < M && col < N)
+          *reinterpret_cast<uint4*>(c + row * p.ldc + col) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+      }
+    }
+    par ^= nt & 1;
+    ra_c = ra_n;
+    rb_c = rb_n;
+    make_rsrc(i + 2, ra_n, rb_n);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 int group_m(int ntm, int ntn) {
   static const int env = [] {
     const char* e = getenv("EMA_GEMM_GM");
@@ -576,14 +924,35 @@ int group_m(int ntm, int ntn) {
 // switches it at run time (A/B in one process).
 int g_variant = [] {
   const char* e = getenv("EMA_GEMM_NT");
-  return (e && e[0] == '8') ? 8 : 4;
+  return e ? (e[0] == '8' ? 8 : e[0] == '4' ? 4 : e[0] == '6' ? 6 : 5) : 5;
 }();
-bool use_wave4() { return g_variant == 4; }
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
 
 template <typename T, int EPI, int ACT>
 void launch_one(const NtArgs& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.ntm * p.ntn));
-  if (use_wave4() && p.K % BK2 == 0 && p.wave4_ok) hipLaunchKernelGGL((gemm_nt4_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
+  if constexpr (EPI == EPI_STORE) {
+    const int64_t lim = (int64_t)1 << 31;
+    if (g_variant == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 && p.am.rows == 0 && p.cm.rows == 0 &&
+        (int64_t)p.M * p.lda * 2 < lim && (int64_t)p.N * p.ldb * 2 < lim) {
+      const int g = std::min(p.ntm * p.ntn, num_cus());
+      hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, p);
+      return;
+    }
+  }
+  const bool w4 = g_variant != 8 && p.K % BK2 == 0 && p.wave4_ok;
+  if (w4 && g_variant == 5) hipLaunchKernelGGL((gemm_nt5_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
+  else if (w4) hipLaunchKernelGGL((gemm_nt4_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt_k<T, EPI, ACT>), grid, dim3(512), 0, s, p);
 }
 
@@ -610,7 +979,7 @@ void launch_nt(NtArgs& p, int kind, int dt, hipStream_t s) {
 
 }  // namespace
 
-void gemm_nt_set_variant(int v) { g_variant = v == 8 ? 8 : 4; }
+void gemm_nt_set_variant(int v) { g_variant = (v == 8 || v == 4 || v == 6) ? v : 5; }
 
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
   return M > 0 && N > 0 && K > 0 && K % BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&

@@ -351,7 +351,7 @@ def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scal
         if writer and args.log_timers_to_tensorboard:
             writer.add_scalar("iteration-time", per_iter, iteration)
         s = f" iteration {iteration:8d}/{args.train_iters:8d} |"
-        s += f" consumed samples: {args.consumed_train_samples:12d} |"
+        s += f" consumed samples: {consumed_samples:12d} |"
         s += f" elapsed time per iteration (ms): {per_iter * 1000.0:.1f} |"
         s += f" learning rate: {learning_rate:.3E} |"
         s += f" global batch size: {batch_size:5d} |"

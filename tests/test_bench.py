@@ -79,7 +79,7 @@ import pytest  # noqa: E402
 @pytest.mark.parametrize("preset,parallel,groups", [
     ("llama7b-tp8-seq4096", "tp8+sp", (1, 8, 1)),
     ("falcon40b-tp4-pp2", "tp4+sp_pp2+vpp1", (1, 4, 2)),
-    ("llama70b-tp8", "tp8+sp+distopt+recompute_budget260gb", (1, 8, 1)),
+    ("llama70b-tp8", "tp8+sp+distopt+recompute_full", (1, 8, 1)),
 ])
 def test_bench_multi_gpu_presets_on_gloo(preset, parallel, groups):
     """The three multi-GPU BASELINE presets run end to end at 8 ranks (the
@@ -89,6 +89,19 @@ def test_bench_multi_gpu_presets_on_gloo(preset, parallel, groups):
     assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == parallel
     assert (rec["dp"], rec["tp"], rec["pp"]) == groups
     assert rec["value"] > 0 and rec["final_loss"] == rec["final_loss"]  # not NaN
+
+
+def test_llama70b_presets_keep_the_reference_recompute():
+    """BASELINE config #5 recomputes every layer; the memory-model
+    policy is a separately labelled preset."""
+    import bench
+    for preset, rc, flag in (("llama70b-tp8", "full", "--recompute_granularity"),
+                             ("llama70b-tp8-budget", "budget260gb",
+                              "--recompute_memory_budget_gb")):
+        a = bench._parse(["--preset", preset])
+        cfg, shape = bench._resolve(a, 8)
+        argv, par = bench._framework_argv(a, cfg, shape, 8, on_gpu=False)
+        assert par["recompute"] == rc and flag in argv
 
 
 def test_proxy_is_one_simulated_tp_rank():

@@ -53,6 +53,32 @@ def test_gemm_nt(M, N, K, dtype):
     assert ((c.float() - ref).abs() <= tol).all()
 
 
+@pytest.mark.parametrize("variant", [4, 6, 8])
+@pytest.mark.parametrize("M,N,K", [
+    (256, 256, 128),       # one tile, two K-steps (the persistent kernel's minimum)
+    (300, 264, 192),       # ragged M and N, odd number of K-steps
+    (1000, 1000, 4096),    # ragged, long K, several tiles per workgroup
+    (4096, 4096, 1024),    # 256 tiles: one round
+    (8448, 4096, 640),     # 528 tiles: a partial last round, odd K-steps per tile
+])
+def test_gemm_nt_variants(variant, M, N, K):
+    """Every kernel variant (4-wave, persistent, 8-wave) on the same data."""
+    torch.manual_seed(1)
+    a = _rand(M, K)
+    b = _rand(N, K, scale=K ** -0.5)
+    C = _ext()
+    C.gemm_nt_set_variant(variant)
+    try:
+        c = C.gemm_nt(a, b)
+        c2 = C.gemm_nt(a, b)
+    finally:
+        C.gemm_nt_set_variant(0)
+    ref = a.float() @ b.float().t()
+    tol = 2 ** -7 * ref.abs() + 2e-2
+    assert ((c.float() - ref).abs() <= tol).all()
+    assert torch.equal(c, c2)
+
+
 def test_gemm_nt_identity_asymmetric():
     """A = I with an asymmetric B exposes any row/col swap of the C-write."""
     n = 256

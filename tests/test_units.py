@@ -325,6 +325,25 @@ def test_validate_args_derivations():
     assert not args.sequence_parallel
 
 
+def test_context_parallel_refuses_attention_dropout():
+    """Ring attention has no attention dropout, so CP > 1 with a non-zero
+    --attention_dropout on the non-flash path is refused."""
+    from epfl_megatron_amd.config.arguments import parse_args, validate_args
+
+    def _args(*extra):
+        a = parse_args(None, ["--num_layers", "2", "--hidden_size", "64",
+                              "--num_attention_heads", "8", "--seq_length", "32",
+                              "--max_position_embeddings", "32", "--micro_batch_size", "1",
+                              "--context_parallel_size", "2", *extra])
+        a.rank, a.world_size = 0, 2
+        return a
+
+    with pytest.raises(AssertionError, match="attention dropout"):
+        validate_args(_args("--attention_dropout", "0.1"), {})
+    validate_args(_args("--attention_dropout", "0.0"), {})
+    validate_args(_args("--attention_dropout", "0.1", "--use_flash_attn"), {})
+
+
 # ------------------------------------------------------ checkpoint / resume
 def _train_save_resume(rank, world, ckdir, phase):
     import finetune
