@@ -1060,6 +1060,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_gemm", &wgrad_gemm);
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
+  m.def("wgrad_set_variant", &ema::wgrad_set_variant);
   m.def("wgrad_plan", &wgrad_plan);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none(),
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},

@@ -466,6 +466,222 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   }
 }
 
+// ---- persistent 4-wave wgrad (the gemm_nt.hip variant-6 structure) ---------
+// 256 (n) x 256 (k) tile, 4 waves as 2 x 2, each 128 x 128 = 8 x 8 MFMA
+// 16x16x32 accumulators (AGPR-pinned asm MFMAs).  Tokens are consumed 64 per
+// K-step: per operand two [32 tok][256] images (a) (one per MFMA k-half) in a
+// 64-KiB slot, 2 slots.  Each K-step runs the early-refill schedule of
+// gemm_nt6_k (A half refilled after BARRIER 1, B half after BARRIER 2, the
+// next step awaited three quarters in), the K-steps of consecutive tiles form
+// one stream (the next tile's first two steps load during the current tile's
+// last two), and the epilogue adds the accumulators to G straight from
+// registers: the MFMA takes (X fragment, dY fragment) so each lane holds 4
+// consecutive k of one n row, a 16-B fp32 read-modify-write.
+// DMA: buffer_load ... lds; the per-tile descriptor starts at the tile's first
+// column and ends at the end of the operand, so a piece is one per-lane VGPR
+// (wave parity variant) plus an SGPR offset (token row block + 128-B column
+// block), and the last rows of a ragged edge read zeros past the buffer end.
+typedef __attribute__((ext_vector_type(4))) float f32x4_;
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr int IMG = 32 * 256 * 2;        // one [32][256] 16-bit image (a)
+constexpr int OPB2 = 2 * IMG;            // operand per K-step (64 tokens)
+constexpr int SLOTB2 = 2 * OPB2;         // dY + X
+
+template <typename T>
+__device__ __forceinline__ void wmfma(f32x4_& acc, typename fa::MT<T>::x8 a, typename fa::MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16))
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+template <typename T>
+__device__ __forceinline__ void wmfma0(f32x4_& acc, typename fa::MT<T>::x8 a, typename fa::MT<T>::x8 b) {
+  if constexpr (__is_same(T, bf16))
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+
+template <typename T, bool ACCUM>
+__global__ void __launch_bounds__(256, 1)
+wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
+         int K, int gn, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
+  typedef typename fa::MT<T>::x8 X8;
+  typedef typename fa::MT<T>::x4 X4;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave >> 1, wk = wave & 1;
+  const int G = gridDim.x, bid = blockIdx.x;
+  if (bid >= ntiles) return;
+  const int nmine = (ntiles - 1 - bid) / G + 1;
+  const int ntn = (N + TN - 1) / TN, ntk = (K + TK - 1) / TK;
+  const int nt = M / 64;  // >= 2 (host-checked)
+
+  // per-lane DMA offset of a piece (rows 8 wave .. of an image, 512 B per row)
+  auto lane_off = [&](int ld) {
+    const int row = (lane >> 2) & 7;
+    const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((2 * wave + ((lane >> 4) & 1)) & 3));
+    return (uint32_t)(row * ld * (int)sizeof(T) + 16 * ch);
+  };
+  const uint32_t voff_a = lane_off(N), voff_b = lane_off(K);
+  const uint32_t srow_a = (uint32_t)(8 * wave * N * (int)sizeof(T));
+  const uint32_t srow_b = (uint32_t)(8 * wave * K * (int)sizeof(T));
+
+  auto tile_org = [&](int i, int64_t& n0, int64_t& k0) {
+    const int base = i * G, rem = min(G, ntiles - base);
+    const int2 tt = tile_of(base + xcd_remap(bid, rem), ntn, ntk, gn);
+    n0 = (int64_t)tt.x * TN;
+    k0 = (int64_t)tt.y * TK;
+  };
+  auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
+    int64_t n0 = 0, k0 = 0, na = 0, nb = 0;
+    if (i < nmine) {
+      tile_org(i, n0, k0);
+      na = ((int64_t)M * N - n0) * (int64_t)sizeof(T);
+      nb = ((int64_t)M * K - k0) * (int64_t)sizeof(T);
+    }
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)(dy + n0), 0, (int)na, 0x00020000);
+    rb = __builtin_amdgcn_make_buffer_rsrc((void*)(x + k0), 0, (int)nb, 0x00020000);
+  };
+  char* const ldsp = lds;
+  // piece i (0..3) of image kh of operand op, K-step s, into slot
+  auto dma = [&](int op, int kh, int i, Rsrc r, int s, int slot) {
+    const int ld = op ? K : N;
+    const uint32_t soff = (uint32_t)((s * 64 + 32 * kh) * ld * (int)sizeof(T)) + (op ? srow_b : srow_a) +
+                          128u * (uint32_t)i;
+    const int dst = slot * SLOTB2 + op * OPB2 + kh * IMG + (4 * wave + i) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
+                                             16, op ? voff_b : voff_a, soff, 0, 0);
+  };
+  // DMA piece q (0..7 dY, 8..15 X) of a K-step
+  auto dmaq = [&](int q, Rsrc ra, Rsrc rb, int s, int slot) {
+    const int op = q >> 3, kh = (q >> 2) & 1, i = q & 3;
+    dma(op, kh, i, op ? rb : ra, s, slot);
+  };
+
+  f32x4_ acc[8][8];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+  uint32_t abase[2][2], bbase[2][2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      abase[par][u] = lds_base + frag_base(128 * wn, par, u, lane);
+      bbase[par][u] = lds_base + OPB2 + frag_base(128 * wk, par, u, lane);
+    }
+  X8 set0[16], set1[16];  // [0..7] dY (n) fragments, [8..15] X (k) fragments
+  auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
+    constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
+    constexpr int FF = F & 7, OFF = KH * IMG + 512 * (FF >> 1);
+    const uint32_t b0 = (F < 8 ? abase[FF & 1][0] : bbase[FF & 1][0]) + so;
+    const uint32_t b1 = (F < 8 ? abase[FF & 1][1] : bbase[FF & 1][1]) + so;
+    const X4 lo = fa::tr_read_imm<OFF, T>(b0), hi = fa::tr_read_imm<OFF, T>(b1);
+    dst[F] = fa::join<T>(lo, hi);
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto mfma4 = [&](X8 (&cur)[16], auto gq, auto zero) {
+    constexpr int GG = decltype(gq)::value;
+    static_for<4>([&](auto q) {
+      constexpr int IDX = 4 * GG + decltype(q)::value, I = IDX / 8, J = IDX % 8;
+      if constexpr (decltype(zero)::value) wmfma0<T>(acc[I][J], cur[8 + J], cur[I]);
+      else wmfma<T>(acc[I][J], cur[8 + J], cur[I]);
+    });
+  };
+
+  Rsrc ra_c, rb_c, ra_n, rb_n;
+  make_rsrc(0, ra_c, rb_c);
+  make_rsrc(1, ra_n, rb_n);
+  static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 0, 0); });
+  static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 1, 1); });
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  static_for<16>([&](auto f) { read_frag(set0, f, K0{}, 0u); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  int par = 0;
+  for (int i = 0; i < nmine; ++i) {
+    auto kstep = [&](int t, auto zero) {
+      const int slot = (t + par) & 1;
+      const uint32_t so = (uint32_t)(slot * SLOTB2), sn = (uint32_t)(SLOTB2 - so);
+      const bool here = t + 2 < nt;
+      const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
+      const int s2 = here ? t + 2 : t + 2 - nt;
+      static_for<32>([&](auto gq) {
+        constexpr int GG = decltype(gq)::value;
+        if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
+        else mfma4(set1, std::integral_constant<int, GG - 16>{}, std::false_type{});
+        if constexpr (GG < 4) {
+          read_frag(set1, std::integral_constant<int, 2 * GG>{}, K1{}, so);
+          read_frag(set1, std::integral_constant<int, 2 * GG + 1>{}, K1{}, so);
+        }
+        if constexpr (GG == 5 || GG == 11) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (GG >= 6 && GG < 14) dmaq(GG - 6, ra, rb, s2, slot);
+        if constexpr (GG >= 6 && GG < 10) {
+          read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
+          read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
+        }
+        if constexpr (GG >= 12 && GG < 20) dmaq(8 + GG - 12, ra, rb, s2, slot);
+        if constexpr (GG == 23) {
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (GG >= 24) {
+          read_frag(set0, std::integral_constant<int, 2 * (GG - 24)>{}, K0{}, sn);
+          read_frag(set0, std::integral_constant<int, 2 * (GG - 24) + 1>{}, K0{}, sn);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    kstep(0, std::true_type{});
+    for (int t = 1; t < nt; ++t) kstep(t, std::false_type{});
+
+    // epilogue: G[n][k .. k+3] (+)= acc, straight from registers
+    fa::mfma_drain();
+    int64_t n0, k0;
+    tile_org(i, n0, k0);
+    const int64_t kc = k0 + 128 * wk + 4 * (lane >> 4);
+    const int64_t nr = n0 + 128 * wn + (lane & 15);
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+      const int64_t n = nr + 16 * ii;
+      f32x4_* row = reinterpret_cast<f32x4_*>(g + n * K + kc);
+      if constexpr (ACCUM) {
+#pragma unroll
+        for (int jh = 0; jh < 8; jh += 4) {
+          f32x4_ o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            o[j] = (n < N && kc + 16 * (jh + j) < K) ? __builtin_nontemporal_load(row + 4 * (jh + j))
+                                                      : f32x4_{0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n < N && kc + 16 * (jh + j) < K)
+              __builtin_nontemporal_store(o[j] + acc[ii][jh + j], row + 4 * (jh + j));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n < N && kc + 16 * j < K) __builtin_nontemporal_store(acc[ii][j], row + 4 * j);
+      }
+    }
+    par ^= nt & 1;
+    ra_c = ra_n;
+    rb_c = rb_n;
+    make_rsrc(i + 2, ra_n, rb_n);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Tile grouping: a few tiles of the SHORTER output dimension x all tiles of
 // the longer one, so an XCD's 32 concurrent workgroups form an 8 x 4 block
 // (measured on the 7B shapes, profiles/r2_wgrad_ab.txt: +3-5 % on qkv / fc1 /
@@ -594,25 +810,55 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
   return pl.nsplit > 1 ? (int64_t)pl.nsplit * pl.tail_tiles * TN * TK : 0;
 }
 
+// Kernel for the whole-tile rounds: 4 = persistent 4-wave wgrad4_k (default),
+// 8 = the 8-wave ping-pong wgrad_k (EMA_WGRAD_V=8 / wgrad_set_variant: A/B).
+int g_wvar = [] {
+  const char* e = getenv("EMA_WGRAD_V");
+  return (e && e[0] == '8') ? 8 : 4;
+}();
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+bool wgrad4_ok(int64_t M, int64_t N, int64_t K) {
+  const int64_t lim = (int64_t)1 << 31;
+  return g_wvar == 4 && M % 64 == 0 && M >= 128 && M * N * 2 < lim && M * K * 2 < lim;
+}
+
+template <typename T, bool ACCUM>
+void launch4(const void* dy, const void* x, float* g, int M, int N, int K, int tiles, hipStream_t s) {
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  hipLaunchKernelGGL((wgrad4_k<T, ACCUM>), dim3(grid), dim3(256), 0, s, (const T*)dy, (const T*)x, g,
+                     M, N, K, tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), tiles);
+}
+
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
                 bool accumulate, int dt, hipStream_t s, float* ws) {
   const int iM = (int)M, iN = (int)N, iK = (int)K;
   const WgradPlan pl = wgrad_plan(M, N, K);
   const bool split = pl.nsplit > 1 && ws != nullptr;
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
-  static const bool sched3 = [] {  // EMA_WGRAD_SCHED=3: the 2 + 2 DMA split (A/B)
-    const char* e = getenv("EMA_WGRAD_SCHED");
-    return e && e[0] == '3';
-  }();
+  if (main_tiles > 0 && wgrad4_ok(M, N, K)) {
+    if (dt == DT_BF16) {
+      if (accumulate) launch4<bf16, true>(dy, x, g, iM, iN, iK, main_tiles, s);
+      else launch4<bf16, false>(dy, x, g, iM, iN, iK, main_tiles, s);
+    } else if (dt == DT_F16) {
+      if (accumulate) launch4<fp16, true>(dy, x, g, iM, iN, iK, main_tiles, s);
+      else launch4<fp16, false>(dy, x, g, iM, iN, iK, main_tiles, s);
+    }
+  } else
   if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (sched3) {
-        if (accumulate) launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-        else launch<bf16, false, 0, 3>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      } else {
-        if (accumulate) launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-        else launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      }
+      if (accumulate) launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     } else if (dt == DT_F16) {
       if (accumulate) launch<fp16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
       else launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
@@ -629,5 +875,7 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
                        pl.nsplit, accumulate ? 1 : 0);
   }
 }
+
+void wgrad_set_variant(int v) { g_wvar = v == 8 ? 8 : 4; }
 
 }  // namespace ema

@@ -92,8 +92,37 @@ def ablation(modes=(0, 1, 2)):
             print(f"ablation round {rnd} mode {mode}: {fl / t / 1e12:.1f} TF/s", flush=True)
 
 
+def variants(rounds=3):
+    """Interleaved A/B (one process, CDNA guide rule 24) of the persistent 4-wave
+    kernel, the 8-wave ping-pong kernel and hipBLASLt on the 7B wgrad shapes."""
+    import statistics
+    C = ext()
+    M = 16384
+    res = {}
+    for name, (N, K) in SHAPES.items():
+        dY = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) - 0.5
+        X = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) - 0.5
+        G = torch.zeros(N, K, device="cuda", dtype=torch.float32)
+        fl = 2.0 * M * N * K
+        r = {"v4": [], "v8": [], "lt": []}
+        for _ in range(rounds):
+            for v in (4, 8):
+                C.wgrad_set_variant(v)
+                r[f"v{v}"].append(fl / _time(lambda: C.wgrad_gemm(dY, X, G, True)) / 1e12)
+            C.wgrad_set_variant(4)
+            r["lt"].append(fl / _time(lambda: C.lt_gemm(dY, True, X, False, G, 1.0, 1.0, -1)) / 1e12)
+        res[name] = {k: round(statistics.median(v), 1) for k, v in r.items()}
+        print(f"{name:8s} v4 {res[name]['v4']:7.1f}  v8 {res[name]['v8']:7.1f}  hipBLASLt "
+              f"{res[name]['lt']:7.1f} TF/s  (v4/v8 x{res[name]['v4'] / res[name]['v8']:.3f})",
+              flush=True)
+        del dY, X, G
+    return res
+
+
 if __name__ == "__main__":
-    if "--ablation" in sys.argv:
+    if "--variants" in sys.argv:
+        variants()
+    elif "--ablation" in sys.argv:
         i = sys.argv.index("--ablation")
         ablation(tuple(int(v) for v in sys.argv[i + 1:]) or (0, 1, 2))
     else:

@@ -605,6 +605,33 @@ def test_wgrad_gemm(M, N, K, dtype):
     assert not C.wgrad_supported(M + 16, N, K)
 
 
+@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("M,N,K", [(128, 256, 256), (1024, 768, 512), (2048, 264, 520),
+                                   (4096, 4096, 1376), (16384, 4096, 4096), (8192, 8448, 2048)])
+def test_wgrad_gemm_variants(variant, M, N, K):
+    """The persistent 4-wave kernel (default) and the 8-wave ping-pong kernel on
+    the same data: ragged edges, several tiles per workgroup, partial rounds."""
+    C = _ext()
+    torch.manual_seed(3)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    g0 = torch.randn(N, K, device=DEV, dtype=torch.float32)
+    C.wgrad_set_variant(variant)
+    try:
+        g = g0.clone()
+        C.wgrad_gemm(dy, x, g, True)
+        g2 = torch.full((N, K), float("nan"), device=DEV)
+        C.wgrad_gemm(dy, x, g2, False)
+        g3 = torch.full((N, K), float("nan"), device=DEV)
+        C.wgrad_gemm(dy, x, g3, False)
+    finally:
+        C.wgrad_set_variant(4)
+    ref = dy.float().t() @ x.float()
+    _close(g, g0 + ref, atol=1e-3 * math.sqrt(M), msg="accumulate")
+    _close(g2, ref, atol=1e-3 * math.sqrt(M), msg="store")
+    assert torch.equal(g2, g3)  # deterministic
+
+
 def test_wgrad_plan():
     """Split-K planning: small grids split every tile, a partial last round of
     <= 128 tiles splits only the tail (7B fc1: 1376 tiles = 5 rounds + 96)."""
