@@ -107,6 +107,9 @@ def _parse(argv=None):
     ap.add_argument("--vpp_layers", type=int, default=None,
                     help="layers per virtual pipeline stage (interleaved 1F1B)")
     ap.add_argument("--recompute", default=None, choices=["selective", "full"])
+    ap.add_argument("--comm_diag", action="store_true",
+                    help="add the per-collective table of one extra timed-collective step "
+                         "(always on at --gpus > 1)")
     ap.add_argument("--recompute_budget_gb", type=float, default=None,
                     help="recompute only what the memory model needs to fit this peak")
     ap.add_argument("--no_sp", action="store_true")
@@ -273,6 +276,39 @@ def _proxy_comm(rep, n, steps, ms_step, busbw_gbs):
             "proxy_ms_per_step_if_comm_not_overlapped": round(ms_step + ms, 2)}
 
 
+def _comm_diag(rep, step_ms):
+    """Per-collective table of one extra (untimed) step with HIP-event timing on:
+    calls, bytes, in-flight ms (issue -> wait), algorithm and bus bandwidth
+    (ring factors over the group's rank count) — so a multi-GPU record says
+    where its time goes without another run (reference: megatron/timers.py:162-203)."""
+    from epfl_megatron_amd.parallel import comm
+    fac = {"all_reduce": lambda n: 2.0 * (n - 1) / n, "all_gather": lambda n: (n - 1) / n,
+           "reduce_scatter": lambda n: (n - 1) / n}
+    per, tot = {}, 0.0
+    for key, (cnt, nbytes, ms) in rep.items():
+        op, _, grp = key.partition("/")
+        n = comm.group_size(grp)
+        d = {"calls": cnt, "MiB": round(nbytes / 2**20, 1), "ms_in_flight": round(ms, 2)}
+        if n:
+            d["ranks"] = n
+        if ms > 0 and nbytes:
+            alg = nbytes / (ms * 1e-3) / 1e9
+            d["algbw_GBs"] = round(alg, 1)
+            if n and op in fac:
+                d["busbw_GBs"] = round(alg * fac[op](n), 1)
+        per[key] = d
+        tot += ms
+    return {"step_ms_with_timing": round(step_ms, 2), "sum_ms_in_flight": round(tot, 2),
+            "collectives": per}
+
+
+def _n1_ref_path(label, par):
+    import tempfile
+    key = f"{label}_s{par['seq']}_mb{par['mbs']}x{par['nmicro']}_tp{par['tp']}pp{par['pp']}cp{par['cp']}"
+    key = "".join(c if c.isalnum() else "_" for c in key)
+    return os.path.join(tempfile.gettempdir(), f"ema_bench_n1_{key}.json")
+
+
 def _label(cfg, shape, a):
     names = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-70b": "Llama-2-70B",
              "falcon-7b": "Falcon-7B", "falcon-40b": "Falcon-40B"}
@@ -376,6 +412,18 @@ def main(argv=None):
     if state.get_pipeline_model_parallel_world_size() > 1:
         src = state.get_pipeline_model_parallel_last_rank()
         dist.broadcast(loss_t, src=src, group=state.get_pipeline_model_parallel_group())
+    diag = None
+    if world > 1 or a.comm_diag:
+        # one more step, untimed, with per-collective HIP-event timing
+        comm.set_timing(True)
+        t1 = time.perf_counter()
+        step()
+        for m in chunks:  # the dist-opt parameter all-gather still in flight
+            if hasattr(m, "wait_param_sync"):
+                m.wait_param_sync()
+        sync()
+        diag = _comm_diag(comm.report(reset=True), (time.perf_counter() - t1) * 1e3)
+        comm.set_timing(False)
     optimizer.resolve_pending()
     tokens = par["gbs"] * par["seq"] * a.steps
     tok_s = tokens / dt
@@ -453,6 +501,25 @@ def main(argv=None):
         if a.proxy:
             rec.update(_proxy_comm(comm_rep, par["sim_tp"], a.steps, 1000.0 * dt / a.steps,
                                    a.xgmi_busbw_gbs))
+        # weak-scaling reference: an N=1 run of the same per-GPU config leaves its
+        # step time behind; an N>1 run reports the step time it lost to N ranks
+        if not a.proxy and par["dp"] >= 1:
+            ref_path = _n1_ref_path(label, par)
+            if world == 1 and on_gpu:
+                try:
+                    with open(ref_path, "w") as f:
+                        json.dump({"ms_per_step": rec["ms_per_step"]}, f)
+                except OSError:
+                    pass
+            elif world > 1 and diag is not None and os.path.exists(ref_path):
+                try:
+                    n1 = json.load(open(ref_path))["ms_per_step"]
+                    diag["n1_ms_per_step"] = n1
+                    diag["exposed_ms_vs_n1"] = round(rec["ms_per_step"] - n1, 2)
+                except (OSError, ValueError, KeyError):
+                    pass
+        if diag is not None:
+            rec["comm_diag"] = diag
         print(json.dumps(rec), flush=True)
     else:
         rec = None

@@ -26,6 +26,7 @@ Two debug/observability aids live here:
   gradients; the CPU tests run with the checker on.
 """
 import os
+import time
 from collections import OrderedDict
 
 import torch
@@ -37,6 +38,7 @@ _CHECK = os.environ.get("EMA_COMM_CHECK", "0") == "1"
 _TIMING = [False]
 _STATS = OrderedDict()  # key -> [count, bytes, ms]
 _GROUP_NAMES = {}
+_GROUP_SIZES = {}  # name -> ranks in the group (bus-bandwidth factors of the report)
 _PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
 _LOOPBACK = {}  # id(group) -> simulated size (--simulated_tensor_parallel_size)
 
@@ -64,6 +66,9 @@ def set_loopback(group, world):
         _LOOPBACK[id(group)] = int(world)
     else:
         _LOOPBACK.pop(id(group), None)
+    name = _GROUP_NAMES.get(id(group))
+    if name is not None and world:
+        _GROUP_SIZES[name] = int(world)
 
 
 def loopback_size(group):
@@ -73,6 +78,15 @@ def loopback_size(group):
 def name_group(group, name):
     """Give a process group a readable name in the accounting table."""
     _GROUP_NAMES[id(group)] = name
+    try:
+        _GROUP_SIZES[name] = _LOOPBACK.get(id(group)) or dist.get_world_size(group)
+    except (RuntimeError, ValueError):
+        pass
+
+
+def group_size(name):
+    """Ranks of the named group (None if unknown)."""
+    return _GROUP_SIZES.get(name)
 
 
 def _key(op, group):
@@ -93,11 +107,18 @@ def _events_on(t):
     return _TIMING[0] and t.is_cuda and not torch.cuda.is_current_stream_capturing()
 
 
+def _add_ms(key, ms):
+    rec = _STATS.get(key)
+    if rec is None:  # e.g. "p2p/.." (bytes are accounted per direction)
+        rec = _STATS[key] = [0, 0, 0.0]
+    rec[2] += ms
+
+
 def _fold_events(block=False):
     keep = []
     for key, s, e in _PENDING_EVENTS:
         if block or e.query():
-            _STATS[key][2] += s.elapsed_time(e)
+            _add_ms(key, s.elapsed_time(e))
         else:
             keep.append((key, s, e))
     _PENDING_EVENTS[:] = keep
@@ -137,11 +158,13 @@ class Work:
     """Handle of an issued collective (``wait()`` makes the result visible to
     the current stream)."""
 
-    __slots__ = ("_work", "_run", "_key", "_start", "_done", "_snap", "_watch")
+    __slots__ = ("_work", "_run", "_key", "_start", "_done", "_snap", "_watch", "_t0")
 
-    def __init__(self, work=None, run=None, key=None, start=None, watch=None, snap=None):
+    def __init__(self, work=None, run=None, key=None, start=None, watch=None, snap=None,
+                 t0=None):
         self._work, self._run, self._key, self._start = work, run, key, start
         self._watch, self._snap = watch, snap
+        self._t0 = t0  # host clock at issue (timing of host-side collectives: gloo)
         self._done = False
 
     def wait(self):
@@ -161,6 +184,12 @@ class Work:
             end = torch.cuda.Event(enable_timing=True)
             end.record()
             _PENDING_EVENTS.append((self._key, self._start, end))
+        elif self._t0 is not None:
+            _add_ms(self._key, (time.perf_counter() - self._t0) * 1e3)
+
+
+def _host_t0(t):
+    return time.perf_counter() if _TIMING[0] and not t.is_cuda else None
 
 
 def _issue(op, group, tensor_for_bytes, watch, fn, async_op):
@@ -178,11 +207,12 @@ def _issue_inner(key, tensor_for_bytes, watch, fn, async_op):
     if _events_on(tensor_for_bytes):
         start = torch.cuda.Event(enable_timing=True)
         start.record()
+    t0 = _host_t0(tensor_for_bytes)
     if async_op and _CHECK:
         return Work(run=lambda: fn(False), key=key, start=start, watch=watch,
-                    snap=watch.detach().clone())
+                    snap=watch.detach().clone(), t0=t0)
     w = fn(async_op)
-    h = Work(work=w, key=key, start=start)
+    h = Work(work=w, key=key, start=start, t0=t0)
     if not async_op:
         h.wait()
         return None
@@ -292,15 +322,16 @@ def _p2p_issue(key, ref, sent, fn, async_op):
     if _events_on(ref):
         start = torch.cuda.Event(enable_timing=True)
         start.record()
+    t0 = _host_t0(ref)
     if async_op and _CHECK and sent:
         # Only pure sends are deferred (a receive must complete before its
         # consumer runs): snapshot the send buffers, verify and send at wait().
         watch = torch.cat([t.detach().reshape(-1).view(torch.uint8) for t in sent]) \
             if len(sent) > 1 else sent[0].detach().reshape(-1).view(torch.uint8)
         return Work(run=lambda: fn(False), key=key, start=start, watch=_SendWatch(sent),
-                    snap=watch.clone())
+                    snap=watch.clone(), t0=t0)
     w = fn(async_op)
-    h = Work(work=w, key=key, start=start)
+    h = Work(work=w, key=key, start=start, t0=t0)
     if not async_op:
         h.wait()
         return None

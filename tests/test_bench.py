@@ -30,6 +30,16 @@ def test_bench_spawns_ranks():
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["value"] > 0 and rec["scaling"] == "weak"
+    # self-diagnosing multi-rank record: per-collective
+    # counts, bytes, in-flight time and bandwidth of one extra timed step
+    diag = rec["comm_diag"]
+    assert diag["step_ms_with_timing"] > 0 and diag["sum_ms_in_flight"] > 0
+    rs = [v for k, v in diag["collectives"].items() if k.startswith("reduce_scatter/dp")]
+    ag = [v for k, v in diag["collectives"].items() if k.startswith("all_gather/dp")]
+    assert rs and ag, diag["collectives"].keys()
+    for d in rs + ag:
+        assert d["calls"] > 0 and d["MiB"] > 0 and d["ranks"] == 4
+        assert d["ms_in_flight"] > 0 and d["busbw_GBs"] > 0
 
 
 def test_bench_single_rank_default():
