@@ -684,50 +684,6 @@ at::Tensor skinny_norm_glu(const at::Tensor& x, const at::Tensor& w1,
   return y;
 }
 
-// The MLP side of a decode layer in one persistent launch (TP = 1):
-// h2 = ctx Wo^T + x; y = glu(rmsnorm(h2) W1^T) W2^T + h2.  sync: int64 [2] on
-// the device, zero-initialised once ([0] the barrier counter, [1] timeouts).
-at::Tensor decode_mlp(const at::Tensor& ctx, const at::Tensor& x, const at::Tensor& wo,
-                      const at::Tensor& ln_w, double eps, const at::Tensor& w1,
-                      const at::Tensor& w2, int64_t kind, at::Tensor sync, int64_t mode) {
-  auto pa = skinny_args(ctx, wo, c10::nullopt, 0.0);
-  const int64_t M = ctx.size(0), H = wo.size(0), F = w2.size(1);
-  TORCH_CHECK(ema::decode_mlp_supported(M, H, F) && ctx.size(1) % 256 == 0 &&
-              ctx.size(1) / 8 >= 256, "decode_mlp: unsupported shape");
-  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == ctx.scalar_type() &&
-              x.dim() == 2 && x.size(0) == M && x.size(1) == H, "decode_mlp: x [M, H]");
-  TORCH_CHECK(w1.dim() == 2 && w1.size(0) == 2 * F && w1.size(1) == H && w2.size(0) == H,
-              "decode_mlp: w1 [2F, H], w2 [H, F]");
-  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 2 &&
-              sync.is_contiguous(), "decode_mlp: sync int64 [2]");
-  check_vec_aligned(x, "x");
-  auto h2 = at::empty({M, H}, ctx.options());
-  auto act = at::empty({M, F}, ctx.options());
-  auto y = at::empty({M, H}, ctx.options());
-  pa.N = (int)H;
-  pa.y = h2.data_ptr();
-  pa.ldy = H;
-  pa.res = x.data_ptr();
-  pa.ldr = H;
-  auto pb = skinny_args(h2, w1, ln_w, eps);
-  pb.N = (int)F;
-  pb.y = act.data_ptr();
-  pb.ldy = F;
-  pb.act = (int)kind;
-  auto pc = skinny_args(act, w2, c10::nullopt, 0.0);
-  pc.N = (int)H;
-  pc.y = y.data_ptr();
-  pc.ldy = H;
-  pc.res = h2.data_ptr();
-  pc.ldr = H;
-  ema::decode_mlp(pa, pb, pc, reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()),
-                  dtype_code(ctx), cur_stream(), (int)mode);
-  return y;
-}
-
-bool decode_mlp_supported(int64_t M, int64_t H, int64_t F) {
-  return ema::decode_mlp_supported(M, H, F);
-}
 
 // qkv decode projection: returns the rotated q [M, ng * r * hd]; k / v rows go
 // to kcache / vcache [L, B, ng, hd] (views at the batch offset) at the slot
@@ -1108,10 +1064,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_norm_gemm", &skinny_norm_gemm);
   m.def("skinny_norm_glu", &skinny_norm_glu);
   m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache);
-  m.def("decode_mlp", &decode_mlp, py::arg("ctx"), py::arg("x"), py::arg("wo"), py::arg("ln_w"),
-        py::arg("eps"), py::arg("w1"), py::arg("w2"), py::arg("kind"), py::arg("sync"),
-        py::arg("mode") = 0);
-  m.def("decode_mlp_supported", &decode_mlp_supported);
   m.def("transpose16", &transpose16);
   m.def("transpose16_supported", &transpose16_supported);
 }

@@ -250,12 +250,6 @@ struct SkinnyArgs {
   int no_halves;        // 1: the persistent GLU keeps full blocks in its last round (A/B)
 };
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
-// one persistent launch for a decode layer's MLP side (TP = 1): pa = dense +
-// residual, pb = RMSNorm + fc1 + GLU, pc = fc2 + residual; grid barriers on
-// sync[0] (a growing 64-bit counter), sync[1] counts barrier timeouts
-bool decode_mlp_supported(int64_t M, int64_t H, int64_t F);
-void decode_mlp(const SkinnyArgs& pa, const SkinnyArgs& pb, const SkinnyArgs& pc,
-                unsigned long long* sync, int dt, hipStream_t s, int mode = 0);
 
 // ---- transpose.hip -------------------------------------------------------------------------------
 // dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.

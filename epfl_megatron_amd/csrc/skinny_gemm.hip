@@ -461,305 +461,9 @@ void dispatch(const SkinnyArgs& p, int epi, hipStream_t s) {
 }
 
 
-// ---------------------------------------------------------------------------
-// The MLP side of a decode layer in ONE persistent launch (batch <= 16,
-// TP = 1):
-//
-//     h2 = ctx · Wo^T + x              (phase A, EPI_RES)
-//     a  = glu(rmsnorm(h2) · W1^T)     (phase B, NORM + EPI_GLU, persistent ring)
-//     y  = a · W2^T + h2               (phase C, EPI_RES)
-//
-// Three launches cost three ramps (first weight bytes ~2-3 us after launch)
-// and three drains.  Here one grid of num_cus() workgroups runs the phases
-// back to back with a grid-wide barrier between them, and each workgroup
-// issues the FIRST weight ring of the next phase before it enters the
-// barrier: weights do not depend on the previous phase, so the stream keeps
-// going through the barrier and only the activation loads wait for it.
-//
-// Barrier (grid_arrive / grid_wait): a 64-bit arrival counter that only grows (no reset between
-// launches or layers): each arrival takes a ticket with a device-scope
-// atomic add; the tickets of one barrier are [e G, (e + 1) G), so the
-// workgroup waits for the counter to reach (ticket / G + 1) G.  All G
-// workgroups are co-resident (G = CUs, 512 threads, one per CU); the wait is
-// bounded anyway: after ~2^18 polls the workgroup records an error in
-// sync[1] and continues (wrong numbers, never a hung GPU).
-// ---------------------------------------------------------------------------
-// arrival: every wave's earlier stores are released to device scope, then
-// thread 0 takes the ticket; returns the count to wait for (thread 0 only)
-__device__ __forceinline__ unsigned long long grid_arrive(unsigned long long* sync,
-                                                          unsigned long long G) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  unsigned long long target = 0;
-  if (threadIdx.x == 0) {
-    const unsigned long long t =
-        __hip_atomic_fetch_add(sync, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    target = (t / G + 1) * G;
-  }
-  return target;
-}
-
-// wait: thread 0 polls (bounded), acquires at device scope (invalidates this
-// CU's caches for the whole workgroup), then the workgroup barrier
-__device__ __forceinline__ void grid_wait(unsigned long long* sync, unsigned long long target) {
-  if (threadIdx.x == 0) {
-    for (int i = 0;; ++i) {
-      if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      if (i > (1 << 18)) {
-        __hip_atomic_fetch_add(sync + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-constexpr int DU = 8;  // ring depth of the block-at-a-time phases (A, C)
-
-// first DU k-steps of W for block `blk` of a block-at-a-time phase
-template <typename T, int EPI>
-__device__ __forceinline__ void dyn_issue(const SkinnyArgs& p, int blk,
-                                          typename fa::MT<T>::x8 (&a)[DU]) {
-  typedef typename fa::MT<T>::x8 x8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nb = EPI == EPI_GLU ? p.N / 8 : p.N / 16;
-  blk = blk < nb ? blk : nb - 1;
-  const int r = lane & 15, kc = 8 * (lane >> 4), kq = p.K / 8;
-  const T* wr = (const T*)p.w + w_row<EPI>(blk, r, p.N) * p.K + wave * kq + kc;
-#pragma unroll
-  for (int u = 0; u < DU; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
-}
-
-// blocks bid, bid + G, ... of Y = X W^T (+ epilogue), 8 waves splitting K,
-// the first block's W ring already issued (dyn_issue); K / 8 >= 32 DU
-template <typename T, int EPI, int ACT>
-__device__ __forceinline__ void dyn_phase(const SkinnyArgs& p, int bid, int G,
-                                          typename fa::MT<T>::x8 (&a)[DU], f4 (*part)[64]) {
-  typedef typename fa::MT<T>::x8 x8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int M = p.M, N = p.N, K = p.K;
-  const int nb = EPI == EPI_GLU ? N / 8 : N / 16;
-  const int kq = K / 8, kbeg = wave * kq;
-  const int r = lane & 15, kc = 8 * (lane >> 4);
-  const bool xon = r < M;
-  const T* xr = (const T*)p.x + (int64_t)(xon ? r : 0) * K + kbeg + kc;
-  const int steps = kq / 32, nblk = steps / DU;
-  for (int blk = bid; blk < nb; blk += G) {
-    const T* wr = (const T*)p.w + w_row<EPI>(blk, r, N) * K + kbeg + kc;
-    if (blk != bid) {
-#pragma unroll
-      for (int u = 0; u < DU; ++u)
-        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
-    }
-    x8 xv[DU];
-#pragma unroll
-    for (int u = 0; u < DU; ++u) xv[u] = *reinterpret_cast<const x8*>(xr + 32 * u);
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < nblk; ++b) {
-      const bool refill = b + 1 < nblk;
-#pragma unroll
-      for (int u = 0; u < DU; ++u) {
-        acc = mfma16x16x32<T>(a[u], xon ? xv[u] : x8{}, acc);
-        if (refill) {
-          const int s = (b + 1) * DU + u;
-          a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * s));
-          xv[u] = *reinterpret_cast<const x8*>(xr + 32 * s);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    {  // leftover k-steps (< DU): loads first, then the MFMAs
-      const int s0 = nblk * DU, left = steps - s0;
-#pragma unroll
-      for (int u = 0; u < DU - 1; ++u)
-        if (u < left) {
-          a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * (s0 + u)));
-          xv[u] = *reinterpret_cast<const x8*>(xr + 32 * (s0 + u));
-        }
-#pragma unroll
-      for (int u = 0; u < DU - 1; ++u)
-        if (u < left) acc = mfma16x16x32<T>(a[u], xon ? xv[u] : x8{}, acc);
-    }
-    part[wave][lane] = acc;
-    __syncthreads();
-    if (wave == 0) {
-      f4 t = part[0][lane];
-#pragma unroll
-      for (int i = 1; i < 8; ++i) t += part[i][lane];  // fixed order
-      epilogue<T, EPI, ACT>(p, blk, t, lane);
-    }
-    __syncthreads();
-  }
-}
-
-// first U k-steps of W of the persistent phase's first block (blk = bid)
-template <typename T, int EPI, int STEPS, int U>
-__device__ __forceinline__ void pg_issue(const SkinnyArgs& p, int bid,
-                                         typename fa::MT<T>::x8 (&a)[U]) {
-  typedef typename fa::MT<T>::x8 x8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nb = EPI == EPI_GLU ? p.N / 8 : p.N / 16;
-  const int blk = bid < nb ? bid : nb - 1;
-  const int r = lane & 15, kc = 8 * (lane >> 4);
-  const T* wr = (const T*)p.w + w_row<EPI>(blk, r, p.N) * p.K + wave * STEPS * 32 + kc;
-#pragma unroll
-  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
-}
-
-// skinny_pgemm_k's body over blocks bid, bid + G, ... with the ring issued
-// by pg_issue (K = 8 x 32 x STEPS)
-template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U>
-__device__ __forceinline__ void pg_phase(const SkinnyArgs& p, int bid, int G,
-                                         typename fa::MT<T>::x8 (&a)[U], f4 (*part)[8][64],
-                                         float (*ssq)[16]) {
-  typedef typename fa::MT<T>::x8 x8;
-  constexpr int WAVES = 8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int M = p.M, N = p.N, K = p.K;
-  const int nblocks = EPI == EPI_GLU ? N / 8 : N / 16;
-  if (bid >= nblocks) return;  // uniform per workgroup
-  const int kbeg = wave * STEPS * 32;
-  const int r = lane & 15, kc = 8 * (lane >> 4);
-  const bool xon = r < M;
-  auto wptr = [&](int blk) { return (const T*)p.w + w_row<EPI>(blk, r, N) * K + kbeg + kc; };
-  int blk = bid;
-  const T* wr = wptr(blk);
-  const T* wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
-  x8 xs[STEPS];
-  {
-    const T* xr = (const T*)p.x + (int64_t)r * K + kbeg + kc;
-    if (xon) {
-#pragma unroll
-      for (int s = 0; s < STEPS; ++s) xs[s] = *reinterpret_cast<const x8*>(xr + 32 * s);
-    } else {
-#pragma unroll
-      for (int s = 0; s < STEPS; ++s) xs[s] = x8{};
-    }
-  }
-  if constexpr (NORM) {
-    const T* gr = (const T*)p.norm_w + kbeg + kc;
-    float ss = 0.f;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)xs[s][e];
-        ss += f * f;
-      }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 16) ssq[wave][lane] = ss;
-    __syncthreads();
-    float tot = 0.f;
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
-    const float rs = rsqrtf(tot / (float)K + p.eps);
-#pragma unroll
-    for (int s0 = 0; s0 < STEPS; s0 += 8) {
-      x8 g[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + i));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const T xn = (T)((float)xs[s0 + i][e] * rs);
-          xs[s0 + i][e] = (T)((float)xn * (float)g[i][e]);
-        }
-        if (!xon) xs[s0 + i] = x8{};
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  auto run_block = [&](auto last_c) {
-    constexpr bool LAST = decltype(last_c)::value;
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      acc = mfma16x16x32<T>(a[s % U], xs[s], acc);
-      if (!LAST || s + U < STEPS) {
-        const T* src = s + U < STEPS ? wr + 32 * (s + U) : wn + 32 * (s + U - STEPS);
-        a[s % U] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(src));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-  };
-  for (int j = 0;; ++j) {
-    const bool last = blk + G >= nblocks;
-    const f4 acc = last ? run_block(std::true_type{}) : run_block(std::false_type{});
-    part[j & 1][wave][lane] = acc;
-    __syncthreads();
-    if (wave == 0) {
-      f4 t = part[j & 1][0][lane];
-#pragma unroll
-      for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][lane];  // fixed order
-      epilogue<T, EPI, ACT>(p, blk, t, lane);
-    }
-    if (last) break;
-    blk += G;
-    wr = wn;
-    wn = wptr(blk + G < nblocks ? blk + G : nblocks - 1);
-  }
-}
-
-template <typename T, int ACT>
-__global__ __launch_bounds__(512) void decode_mlp_k(const SkinnyArgs pa, const SkinnyArgs pb,
-                                                    const SkinnyArgs pc,
-                                                    unsigned long long* sync, int mode) {
-  typedef typename fa::MT<T>::x8 x8;
-  constexpr int PU = 16;
-  __shared__ f4 part[2][8][64];
-  __shared__ float ssq[8][16];
-  const int G = (int)gridDim.x, bid = blockIdx.x;
-  x8 a[DU];
-  dyn_issue<T, EPI_RES>(pa, bid, a);
-  dyn_phase<T, EPI_RES, 0>(pa, bid, G, a, part[0]);
-  // the next phase's first weight ring is issued between arrival and wait:
-  // after the release (which drains this wave's memory operations), so the
-  // loads stay in flight while the workgroup waits for the grid
-  // mode (diagnostics, wrong results): bit 0 skips the waits, bit 1 the arrivals
-  x8 b[PU];
-  unsigned long long t = (mode & 2) ? 0 : grid_arrive(sync, (unsigned long long)G);
-  pg_issue<T, EPI_GLU, 16, PU>(pb, bid, b);
-  if (!(mode & 1)) grid_wait(sync, t);
-  pg_phase<T, true, EPI_GLU, ACT, 16, PU>(pb, bid, G, b, part, ssq);
-  t = (mode & 2) ? 0 : grid_arrive(sync, (unsigned long long)G);
-  dyn_issue<T, EPI_RES>(pc, bid, a);
-  if (!(mode & 1)) grid_wait(sync, t);
-  dyn_phase<T, EPI_RES, 0>(pc, bid, G, a, part[0]);
-}
-
-template <typename T>
-void launch_decode_mlp(const SkinnyArgs& pa, const SkinnyArgs& pb, const SkinnyArgs& pc,
-                       unsigned long long* sync, int mode, hipStream_t s) {
-  const dim3 g((unsigned)num_cus()), blk(512);
-  switch (pb.act) {
-    case 0: hipLaunchKernelGGL((decode_mlp_k<T, 0>), g, blk, 0, s, pa, pb, pc, sync, mode); break;
-    case 1: hipLaunchKernelGGL((decode_mlp_k<T, 1>), g, blk, 0, s, pa, pb, pc, sync, mode); break;
-    case 2: hipLaunchKernelGGL((decode_mlp_k<T, 2>), g, blk, 0, s, pa, pb, pc, sync, mode); break;
-    default: hipLaunchKernelGGL((decode_mlp_k<T, 3>), g, blk, 0, s, pa, pb, pc, sync, mode); break;
-  }
-}
 
 }  // namespace
 
-bool decode_mlp_supported(int64_t M, int64_t H, int64_t F) {
-  // phase B keeps the normed X slice in registers: H = 8 x 32 x 16; phases
-  // A / C need K / 8 to hold at least one ring (32 DU elements)
-  return M >= 1 && M <= 16 && H == 4096 && F % 16 == 0 && F / 8 >= 32 * DU && F % 256 == 0;
-}
-
-void decode_mlp(const SkinnyArgs& pa, const SkinnyArgs& pb, const SkinnyArgs& pc,
-                unsigned long long* sync, int dt, hipStream_t s, int mode) {
-  if (dt == DT_BF16) launch_decode_mlp<bf16>(pa, pb, pc, sync, mode, s);
-  else launch_decode_mlp<fp16>(pa, pb, pc, sync, mode, s);
-}
-
-namespace {
-}  // namespace
 
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
   return M >= 1 && M <= 16 && N % 16 == 0 && K % 128 == 0 && N > 0 && K > 0 &&

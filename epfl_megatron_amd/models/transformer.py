@@ -68,22 +68,6 @@ def _make_norm(args, dim=None):
                                sequence_parallel=args.sequence_parallel)
 
 
-# fused decode MLP side in one persistent launch with grid barriers
-# (EMA_DECODE_MLP=1).  Off by default: the device-wide barriers cost more
-# than the launches they remove (profiles/r3x_decode_mlp_fused.txt)
-_DECODE_MLP_FUSED = os.environ.get("EMA_DECODE_MLP", "0") == "1"
-_DECODE_SYNC = {}
-
-
-def _decode_sync(device):
-    """Per-device grid-barrier counter of the fused decode MLP kernel
-    ([0] grows by 2 x grid per launch, never reset; [1] barrier timeouts)."""
-    t = _DECODE_SYNC.get(device)
-    if t is None:
-        t = _DECODE_SYNC[device] = torch.zeros(2, dtype=torch.int64, device=device)
-    return t
-
-
 class DropPath(MegatronModule):
     """Per-sample stochastic depth on ``[s, b, h]``."""
 
@@ -541,15 +525,8 @@ class ParallelTransformerLayer(MegatronModule):
         # all-reduce of [b, H] yields partial sums + residual (reference
         # RowParallelLinear + bias-dropout-add: megatron/model/transformer.py:
         # 707-730, megatron/core/tensor_parallel/layers.py:665-701).
-        F = mlp.dense_4h_to_h.weight.shape[1]
-        if state.get_tensor_model_parallel_world_size() == 1 and _DECODE_MLP_FUSED and \
-                C.decode_mlp_supported(b, H, F) and o.shape[-1] * o.shape[-2] == H:
-            # dense + residual, RMSNorm + fc1 + GLU, fc2 + residual: one
-            # persistent launch with grid barriers (csrc/skinny_gemm.hip decode_mlp_k)
-            y = C.decode_mlp(o.reshape(b, -1), x, sa.dense.weight, ln2.weight, ln2.eps,
-                             mlp.dense_h_to_4h.weight, mlp.dense_4h_to_h.weight,
-                             tp.layers._GLU_KIND[mlp.glu_activation], _decode_sync(x.device))
-            return y.view(1, b, H)
+        # (one persistent launch with grid barriers for these three products was
+        # measured 2.6x slower than the three launches: profiles/r3x_decode_mlp_fused.txt)
         first = state.get_tensor_model_parallel_rank() == 0
         h2 = C.skinny_norm_gemm(o.reshape(b, -1), sa.dense.weight, None, 0.0, x if first else None)
         h2 = tp.reduce_from_tensor_model_parallel_region(h2)

@@ -7,9 +7,10 @@ not split.
 
 MI355X-specific design of the GEMM path (``_LinearFn``):
 
-* Forward and dgrad GEMMs run on hipBLASLt through PyTorch (``EMA_GEMM=tuned``
-  switches to ``ops/gemm.py``'s per-shape solution timing); the wgrad GEMM
-  on the hand-written MFMA kernel (``EMA_WGRAD=hipblaslt`` for the library).
+* Forward and dgrad GEMMs run on hipBLASLt through PyTorch, or on the
+  hand-written NT GEMM (``csrc/gemm_nt.hip``) where its epilogue fuses work;
+  the wgrad GEMM on the hand-written MFMA kernel (``EMA_WGRAD=hipblaslt`` for
+  the library).
 * With ``gradient_accumulation_fusion`` the weight gradient is a
   bf16 x bf16 -> fp32 GEMM written **in place** into the fp32 ``main_grad``
   view of the DDP bucket —
@@ -43,7 +44,6 @@ from .mappings import (copy_to_tensor_model_parallel_region,
 from .random import get_cuda_rng_tracker
 from .utils import VocabUtility
 from ...ops._ext import ext
-from ...ops import gemm as tuned_gemm
 
 _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {
     "tensor_model_parallel": False,
@@ -168,20 +168,12 @@ _WGRAD_KERNEL = os.environ.get("EMA_WGRAD", "hip").lower() == "hip"
 # 7B/70B projections) the kernel splits the tokens over up to 8 workgroups per
 # tile (fp32 partials + ordered reduce).  Under 32 tiles hipBLASLt is used.
 _WGRAD_MIN_TILES = int(os.environ.get("EMA_WGRAD_MIN_TILES", "32"))
-# EMA_GEMM=tuned routes all three products through ops/gemm.py (per-shape
-# solution timing).  Off by default: in the full 7B step it measured 22.4k vs
-# 22.9k tokens/s for PyTorch's own hipBLASLt calls (profiles/r1_gemm_ab.txt) —
-# isolated timings with hot caches do not predict in-model kernel times.
-_TUNED_GEMM = os.environ.get("EMA_GEMM", "torch").lower() == "tuned"
 # Operand layouts: hipBLASLt runs "TN" problems (both operands contiguous
 # along the reduction dim) 15-20 % faster than the forms PyTorch issues for
 # dgrad / wgrad (profiles/r1_gemm_layouts_hipblaslt.json).  EMA_DGRAD_WT=1
 # (default) keeps a K-contiguous copy of every weight, rebuilt once per
 # training step by csrc/transpose.hip, so dX = dY (W^T)^T is a TN GEMM.
-# EMA_WGRAD_TN=1 also transposes dY and X so that
-# main_grad (+)= (dY^T) (X^T)^T is one.
 _DGRAD_WT = os.environ.get("EMA_DGRAD_WT", "1") != "0"
-_WGRAD_TN = os.environ.get("EMA_WGRAD_TN", "0") == "1"
 _WEIGHT_T_GEN = [0]  # 0: no training step in flight -> no cached transposes
 
 
@@ -242,13 +234,6 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
                 and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K) \
                 and (-(-N // 256)) * (-(-K // 256)) >= _WGRAD_MIN_TILES:
             ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
-        elif _TUNED_GEMM:
-            tuned_gemm.wgrad(main_grad.view(N, K), grad_output_2d, input_2d, accumulate)
-        elif _WGRAD_TN and _tn_ok(grad_output_2d) and _tn_ok(input_2d):
-            # token-contiguous operands: dY^T [N, M] and X^T [K, M] -> TN GEMM
-            torch.addmm(main_grad, _transpose(grad_output_2d), _transpose(input_2d).t(),
-                        beta=1.0 if accumulate else 0.0, out_dtype=torch.float32,
-                        out=main_grad)
         else:
             torch.addmm(main_grad, grad_output_2d.t(), input_2d, beta=1.0 if accumulate else 0.0,
                         out_dtype=torch.float32, out=main_grad)
@@ -405,8 +390,6 @@ def sp_gemm_reducescatter(x_full, w):
 
 def _dgrad(g2, weight):
     """dX = dY W: the NT kernel on the per-step cached W^T when it applies."""
-    if g2.is_cuda and _TUNED_GEMM:
-        return tuned_gemm.linear_dgrad(g2, weight)
     wt = _weight_t(weight) if g2.is_cuda else None
     if wt is None:
         return g2.matmul(weight)
@@ -414,8 +397,6 @@ def _dgrad(g2, weight):
 
 
 def _fwd(x2, weight):
-    if x2.is_cuda and _TUNED_GEMM:
-        return tuned_gemm.linear_fwd(x2, weight)
     return gemm(x2, weight) if (_NT_GEMM and x2.is_cuda) else x2.matmul(weight.t())
 
 

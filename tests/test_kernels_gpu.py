@@ -679,24 +679,6 @@ def test_linear_wgrad_fresh_and_accumulate():
     _close(w.main_grad, ref, atol=0.05, msg="main_grad")
 
 
-def test_tuned_gemm_products(tmp_path, monkeypatch):
-    """ops/gemm.py: tuned forward/dgrad/wgrad agree with fp32 references."""
-    monkeypatch.setenv("EMA_GEMM_CACHE", str(tmp_path))
-    from epfl_megatron_amd.ops import gemm
-    torch.manual_seed(3)
-    x = torch.randn(512, 256, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(384, 256, device=DEV, dtype=torch.bfloat16)
-    dy = torch.randn(512, 384, device=DEV, dtype=torch.bfloat16)
-    _close(gemm.linear_fwd(x, w), x.float() @ w.float().t(), atol=0.5, rtol=2e-2, msg="fwd")
-    _close(gemm.linear_dgrad(dy, w), dy.float() @ w.float(), atol=0.5, rtol=2e-2, msg="dgrad")
-    g = torch.full((384, 256), float("nan"), device=DEV)
-    gemm.wgrad(g, dy, x, False)
-    ref = dy.float().t() @ x.float()
-    _close(g, ref, atol=0.05, rtol=1e-3, msg="wgrad store")
-    gemm.wgrad(g, dy, x, True)
-    _close(g, 2 * ref, atol=0.1, rtol=1e-3, msg="wgrad accumulate")
-
-
 @pytest.mark.parametrize("R,C", [(64, 64), (128, 320), (4096, 704)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_transpose16(R, C, dtype):
@@ -710,12 +692,10 @@ def test_transpose16(R, C, dtype):
     assert C_.transpose16_supported(R, C) and not C_.transpose16_supported(R + 32, C)
 
 
-@pytest.mark.parametrize("wgrad_tn", [False, True])
-def test_linear_tn_layouts(monkeypatch, wgrad_tn):
-    """dgrad through the cached W^T (and wgrad through transposed operands) equals the
-    plain products; a new training-step generation picks up an updated weight."""
+def test_linear_tn_layouts(monkeypatch):
+    """dgrad through the cached W^T equals the plain product; a new
+    training-step generation picks up an updated weight."""
     from epfl_megatron_amd.parallel.tensor import layers as L
-    monkeypatch.setattr(L, "_WGRAD_TN", wgrad_tn)
     monkeypatch.setattr(L, "_DGRAD_WT", True)
     torch.manual_seed(4)
     w = torch.nn.Parameter(torch.randn(384, 256, device=DEV, dtype=torch.bfloat16) * 0.05)
@@ -894,45 +874,6 @@ def test_ring_pair_kernels_on_sequence_major_views():
                        causal, hd ** -0.5)
         for a, c in zip(g1, g2):
             assert torch.equal(a, c)
-
-
-@pytest.mark.parametrize("M", [1, 3, 8, 16])
-@pytest.mark.parametrize("F,kind", [(11008, 0), (5632, 1)])
-def test_decode_mlp_fused(M, F, kind):
-    """decode_mlp_k (csrc/skinny_gemm.hip): dense + residual, RMSNorm + fc1 +
-    GLU and fc2 + residual in one persistent launch with grid barriers equals
-    the three skinny launches bit for bit (same K split and summation order),
-    and the fp32 reference within bf16 tolerance; the barrier counter grows by
-    exactly 2 x grid per launch and records no timeout."""
-    C = _ext()
-    torch.manual_seed(M + F)
-    H, dt = 4096, torch.bfloat16
-    ctx = torch.randn(M, H, device=DEV, dtype=dt)
-    x = torch.randn(M, H, device=DEV, dtype=dt)
-    wo = (torch.randn(H, H, device=DEV) * H ** -0.5).to(dt)
-    w1 = (torch.randn(2 * F, H, device=DEV) * H ** -0.5).to(dt)
-    w2 = (torch.randn(H, F, device=DEV) * F ** -0.5).to(dt)
-    g = (1 + 0.1 * torch.randn(H, device=DEV)).to(dt)
-    assert C.decode_mlp_supported(M, H, F)
-    sync = torch.zeros(2, dtype=torch.int64, device=DEV)
-    y = C.decode_mlp(ctx, x, wo, g, 1e-5, w1, w2, kind, sync)
-    y2 = C.decode_mlp(ctx, x, wo, g, 1e-5, w1, w2, kind, sync)
-    torch.cuda.synchronize()
-    grid = torch.cuda.get_device_properties(0).multi_processor_count
-    assert sync[1].item() == 0, "grid barrier timed out"
-    assert sync[0].item() == 4 * grid
-    h2 = C.skinny_norm_gemm(ctx, wo, None, 0.0, x)
-    a = C.skinny_norm_glu(h2, w1, g, 1e-5, kind)
-    ref3 = C.skinny_norm_gemm(a, w2, None, 0.0, h2)
-    assert torch.equal(y, ref3) and torch.equal(y2, ref3)
-    # fp32 reference
-    h2f = ctx.float() @ wo.float().t() + x.float()
-    hn = h2f * torch.rsqrt(h2f.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
-    u, v = (hn @ w1.float().t()).chunk(2, dim=-1)
-    act = {0: torch.nn.functional.silu, 1: torch.nn.functional.gelu}
-    af = u * act[kind](v)
-    yf = af @ w2.float().t() + h2f
-    _close(y, yf, 0.1, 3e-2, "decode_mlp vs fp32")
 
 
 def test_rope_qkv_autograd_matches_reference():
