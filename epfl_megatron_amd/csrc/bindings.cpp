@@ -965,7 +965,7 @@ std::vector<at::Tensor> gemm_nt_glu(const at::Tensor& a, const at::Tensor& w1, i
 // fc2 dgrad with the GLU backward fused: d(pre) [M, 2F] from dy [M, K] and
 // w2t = W2^T [F, K] and the saved pre-activation [M, 2F]
 at::Tensor gemm_nt_dglu(const at::Tensor& dy, const at::Tensor& w2t, const at::Tensor& pre,
-                        int64_t kind) {
+                        int64_t kind, c10::optional<at::Tensor> out) {
   check_gpu(dy, "dy");
   check_rows(dy, "dy");
   check_rows(w2t, "w2t");
@@ -979,7 +979,16 @@ at::Tensor gemm_nt_dglu(const at::Tensor& dy, const at::Tensor& w2t, const at::T
   check_vec_aligned(pre, "pre");
   TORCH_CHECK(ema::gemm_nt_supported(M, F, K, dy.stride(0), w2t.stride(0), 2 * F),
               "gemm_nt_dglu: unsupported shape (K % 32, F % 8)");
-  auto dpre = at::empty({M, 2 * F}, dy.options());
+  at::Tensor dpre;
+  if (out.has_value()) {
+    dpre = *out;
+    TORCH_CHECK(dpre.is_contiguous() && dpre.dim() == 2 && dpre.size(0) == M &&
+                    dpre.size(1) == 2 * F && dpre.scalar_type() == dy.scalar_type(),
+                "gemm_nt_dglu: out must be contiguous [M, 2F] of the operand dtype");
+    check_vec_aligned(dpre, "out");
+  } else {
+    dpre = at::empty({M, 2 * F}, dy.options());
+  }
   ema::gemm_nt_dglu(dy.data_ptr(), w2t.data_ptr(), pre.data_ptr(), dpre.data_ptr(), M, F, K,
                     dy.stride(0), w2t.stride(0), (int)kind, dt, cur_stream());
   return dpre;
@@ -1026,7 +1035,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_glu", &gemm_nt_glu, py::arg("a"), py::arg("w1"), py::arg("kind"),
         py::arg("pre") = py::none(), py::arg("y") = py::none(),
         py::arg("c_map") = std::vector<int64_t>{});
-  m.def("gemm_nt_dglu", &gemm_nt_dglu);
+  m.def("gemm_nt_dglu", &gemm_nt_dglu, py::arg("dy"), py::arg("w2t"), py::arg("pre"),
+        py::arg("kind"), py::arg("out") = py::none());
   m.doc() = "epfl_megatron_amd gfx950 (MI355X) HIP kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("w"), py::arg("eps"),
         py::arg("res") = py::none());

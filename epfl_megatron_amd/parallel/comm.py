@@ -41,6 +41,7 @@ _GROUP_NAMES = {}
 _GROUP_SIZES = {}  # name -> ranks in the group (bus-bandwidth factors of the report)
 _PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
 _LOOPBACK = {}  # id(group) -> simulated size (--simulated_tensor_parallel_size)
+_LOOPBACK_FILLED = set()  # (data_ptr, numel) of all-gather outputs zero-filled once
 
 
 class CommRaceError(RuntimeError):
@@ -58,10 +59,14 @@ def set_timing(enabled):
 
 def set_loopback(group, world):
     """Make ``group`` (a real 1-rank group) stand for ``world`` ranks: its
-    collectives run as local copies with a real rank's traffic accounted —
-    all-gather replicates the input ``world`` times, reduce-scatter writes the
-    mean of the ``world`` chunks, all-reduce / broadcast are identities.  Used
-    by the one-GPU per-rank proxies of the TP configurations."""
+    collectives are accounted with a real rank's bytes but move (almost) none,
+    so the proxy's timed step holds no emulation kernels a real rank would not
+    run: all-gather writes only this rank's own shard into
+    its slot (the other ranks' slots are zero-filled once per buffer and then
+    left as they are — finite stand-ins for the bytes xGMI would deliver),
+    reduce-scatter writes this rank's own chunk (no reduction), all-reduce /
+    broadcast are identities.  Used by the one-GPU per-rank proxies of the TP
+    configurations; the numbers they train on are not a real TP run's."""
     if world and world > 1:
         _LOOPBACK[id(group)] = int(world)
     else:
@@ -246,7 +251,9 @@ def reduce_scatter_into(output, inp, group=None, async_op=False, op="sum"):
     n = _LOOPBACK.get(id(group))
     if n:
         def loop(a):
-            torch.mean(src.view(n, *output.shape), dim=0, out=output)
+            own = src.view(n, *output.shape)[0]
+            if output.data_ptr() != own.data_ptr():
+                output.copy_(own)
         return _issue("reduce_scatter", group, src, src, loop, async_op)
     return _issue("reduce_scatter", group, src, src,
                   lambda a: dist.reduce_scatter_tensor(output, src, op=rop, group=group,
@@ -260,7 +267,13 @@ def all_gather_into(output, inp, group=None, async_op=False):
     n = _LOOPBACK.get(id(group))
     if n:
         def loop(a):
-            output.view(n, *src.shape).copy_(src.unsqueeze(0).expand(n, *src.shape))
+            key = (output.data_ptr(), output.numel())
+            if key not in _LOOPBACK_FILLED:
+                _LOOPBACK_FILLED.add(key)
+                output.zero_()
+            own = output.view(n, *src.shape)[0]
+            if own.data_ptr() != src.data_ptr():
+                own.copy_(src)
         return _issue("all_gather", group, output, src, loop, async_op)
     return _issue("all_gather", group, output, src,
                   lambda a: dist.all_gather_into_tensor(output, src, group=group, async_op=a),

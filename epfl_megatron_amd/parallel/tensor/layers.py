@@ -302,10 +302,11 @@ def gemm_glu(a, w1, kind, pre=None, y=None, c_map=None):
     return pre, y
 
 
-def gemm_dglu(g, w2t, pre, kind):
-    """d(pre) = GLU backward of dAct = g @ w2t^T at the saved pre-activation."""
+def gemm_dglu(g, w2t, pre, kind, out=None):
+    """d(pre) = GLU backward of dAct = g @ w2t^T at the saved pre-activation
+    (written into ``out`` [M, 2F] when given)."""
     if _kernel_ok(g, w2t):
-        return ext().gemm_nt_dglu(g, w2t, pre, kind)
+        return ext().gemm_nt_dglu(g, w2t, pre, kind, out)
     da = g @ w2t.t()
     f = w2t.shape[0]
     x1, x2 = pre[:, :f], pre[:, f:]
@@ -313,7 +314,11 @@ def gemm_dglu(g, w2t, pre, kind):
         xg = x2.detach().requires_grad_()
         a = _act(kind, xg)
         (dact,) = torch.autograd.grad(a, xg, da * x1)
-    return torch.cat([da * _act(kind, x2), dact], dim=-1)
+    res = torch.cat([da * _act(kind, x2), dact], dim=-1)
+    if out is None:
+        return res
+    out.copy_(res)
+    return out
 
 
 # ---- sequence-parallel forward overlap --------------------------------------
@@ -504,9 +509,35 @@ class _RowParallelSPFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         input_, weight = ctx.saved_tensors
-        full = gather_along_first_dim(grad_output.contiguous())
-        gi, gw, _ = _linear_backward(input_, weight, full, False, ctx.gaf, False, False)
-        return gi, gw, None
+        world, group = _tp()
+        g_local = grad_output.reshape(-1, grad_output.shape[-1])
+        if not g_local.is_contiguous():
+            g_local = g_local.contiguous()
+        rl, H = g_local.shape
+        c = _sp_pieces(rl)
+        if c == 1:
+            full = gather_along_first_dim(grad_output.contiguous())
+            gi, gw, _ = _linear_backward(input_, weight, full, False, ctx.gaf, False, False)
+            return gi, gw, None
+        # dY all-gather in c pieces, each overlapping the previous piece's dgrad
+        # (the reference gathers dY in one blocking collective before any GEMM:
+        # megatron/core/tensor_parallel/mappings.py:244-246).  Piece j arrives
+        # rank-major; its dgrad rows go to their natural [s, b] rows by the
+        # GEMM's row map, and the wgrad pairs it with X in the same piece order.
+        R = rl // c
+        g = get_global_memory_buffer().get_tensor((c, world * R, H), g_local.dtype, "mpu_dy")
+        works = [comm.all_gather_into(g[j], g_local[j * R:(j + 1) * R], group=group,
+                                      async_op=True) for j in range(c)]
+        x2 = input_.reshape(-1, input_.shape[-1])
+        K = x2.shape[1]
+        gi = torch.empty(world * rl, K, dtype=x2.dtype, device=x2.device)
+        wt = _weight_t_always(weight)
+        for j in range(c):
+            works[j].wait()
+            gemm(g[j], wt, gi, c_map=(R, c * R, j * R))
+        xp = x2.view(world, c, R, K).transpose(0, 1).reshape(c * world * R, K)
+        gw = _wgrad(weight, g.view(-1, H), xp, ctx.gaf)
+        return gi.view(*input_.shape), gw, None
 
 
 # Fused GLU MLP (column-parallel fc1 -> GLU -> row-parallel fc2) on the hand-
@@ -556,8 +587,7 @@ class _GluMLPFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         if sequence_parallel:
-            pre, y = sp_allgather_gemm(x2, w1, glu_kind=kind)
-            out = sp_gemm_reducescatter(y, w2)
+            pre, y, out = _sp_mlp_forward(x2, w1, w2, kind)
             lead = tuple(input_.shape[:-1])
         else:
             pre, y = gemm_glu(x2, w1, kind)
@@ -576,23 +606,17 @@ class _GluMLPFn(torch.autograd.Function):
         g2 = grad_out.reshape(-1, grad_out.shape[-1])
         if not g2.is_contiguous():
             g2 = g2.contiguous()
-        gather_handle = None
         if ctx.sp:
-            g2 = gather_along_first_dim(g2)  # dOut of every rank's rows
-            shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
-            total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
-            gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
-        else:
-            total = input_
+            dx, gw1, gw2 = _sp_mlp_backward(input_, g2, w1, w2, pre, y, ctx.kind, ctx.gaf)
+            return dx.view(*input_.shape), gw1, gw2, None, None, None, None
+        gather_handle = None
+        total = input_
         # fc2 dgrad with the GLU backward in the epilogue: d(pre-act) [M, 2F]
         dpre = gemm_dglu(g2, _weight_t_always(w2), pre, ctx.kind)
         # fc1 dgrad: dX = d(pre) W1 = d(pre) (W1^T)^T
         dx = gemm(dpre, _weight_t_always(w1)).view(*total.shape[:-1], w1.shape[1])
-        handle, sub = None, None
-        if ctx.sp:
-            sub = torch.empty_like(input_)
-            handle = comm.reduce_scatter_into(sub, dx, group=tp_group, async_op=True)
-        elif ctx.tp_async and tp_group is not None:
+        handle = None
+        if ctx.tp_async and tp_group is not None:
             handle = comm.all_reduce(dx, group=tp_group, async_op=True)
         # weight gradients while the dX collective runs
         gw2 = _wgrad(w2, g2, y, ctx.gaf)
@@ -602,7 +626,85 @@ class _GluMLPFn(torch.autograd.Function):
         gw1 = _wgrad(w1, dpre, x2, ctx.gaf)
         if handle is not None:
             handle.wait()
-        return (sub if ctx.sp else dx), gw1, gw2, None, None, None, None
+        return dx, gw1, gw2, None, None, None, None
+
+
+# Sequence-parallel GLU MLP in "piece-major" row order.  The local rows are
+# cut into c pieces; piece j is all-gathered on its own ([tp][R] rows, rank-
+# major) and carried through fc1 + GLU -> fc2 -> reduce-scatter as it is: the
+# reduce-scatter of a rank-major [tp][R] product hands every rank exactly its
+# own R rows of piece j, so no GEMM needs a row remap and the token order the
+# MLP sees (irrelevant to it) is (piece, rank, row).  The saved pre-activation
+# and GLU output stay in that order; the backward gathers dOut and the input in
+# the same pieces, so dW sums pair matching rows.  Collectives of piece j+1 run
+# on RCCL's stream while piece j computes.  Reference (blocking forms):
+# megatron/core/tensor_parallel/layers.py:225-243, mappings.py:107-124, 244-246.
+def _sp_mlp_forward(x_local, w1, w2, kind):
+    world, group = _tp()
+    rl, H = x_local.shape
+    c = _sp_pieces(rl)
+    R = rl // c
+    dt, dev = x_local.dtype, x_local.device
+    F = w2.shape[1]
+    g = get_global_memory_buffer().get_tensor((c, world * R, H), dt, "mpu")
+    works = [comm.all_gather_into(g[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
+             for j in range(c)]
+    pre = torch.empty(c, world * R, 2 * F, dtype=dt, device=dev)
+    y = torch.empty(c, world * R, F, dtype=dt, device=dev)
+    part = torch.empty(c, world * R, w2.shape[0], dtype=dt, device=dev)
+    out = torch.empty(rl, w2.shape[0], dtype=dt, device=dev)
+    rs = []
+    for j in range(c):
+        works[j].wait()
+        gemm_glu(g[j], w1, kind, pre[j], y[j])
+        gemm(y[j], w2, part[j])
+        rs.append(comm.reduce_scatter_into(out[j * R:(j + 1) * R], part[j], group=group,
+                                           async_op=True))
+    for w in rs:
+        w.wait()
+    return pre.view(c * world * R, 2 * F), y.view(c * world * R, F), out
+
+
+def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf):
+    """Backward of ``_sp_mlp_forward``: dOut and X gathered in the forward's
+    pieces; per piece the fc2 dgrad (+ GLU backward) and the fc1 dgrad run while
+    the next piece's gathers fly, and dX's reduce-scatter of piece j overlaps
+    piece j+1; both wgrads run last over all pieces."""
+    world, group = _tp()
+    x_local = input_.reshape(-1, input_.shape[-1])
+    if not x_local.is_contiguous():
+        x_local = x_local.contiguous()
+    rl, H = x_local.shape
+    c = _sp_pieces(rl)
+    R = rl // c
+    dt, dev = x_local.dtype, x_local.device
+    F = w2.shape[1]
+    buf = get_global_memory_buffer()
+    g2 = buf.get_tensor((c, world * R, g_local.shape[1]), g_local.dtype, "mpu_dy")
+    gw = [comm.all_gather_into(g2[j], g_local[j * R:(j + 1) * R], group=group, async_op=True)
+          for j in range(c)]
+    xt = buf.get_tensor((c, world * R, H), dt, "mpu")
+    xw = [comm.all_gather_into(xt[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
+          for j in range(c)]
+    pre3 = pre.view(c, world * R, 2 * F)
+    dpre = torch.empty(c, world * R, 2 * F, dtype=dt, device=dev)
+    dxp = torch.empty(c, world * R, H, dtype=dt, device=dev)
+    dx = torch.empty(rl, H, dtype=dt, device=dev)
+    w2t, w1t = _weight_t_always(w2), _weight_t_always(w1)
+    rs = []
+    for j in range(c):
+        gw[j].wait()
+        gemm_dglu(g2[j], w2t, pre3[j], kind, dpre[j])
+        gemm(dpre[j], w1t, dxp[j])
+        rs.append(comm.reduce_scatter_into(dx[j * R:(j + 1) * R], dxp[j], group=group,
+                                           async_op=True))
+    gw2 = _wgrad(w2, g2.view(c * world * R, -1), y, gaf)
+    for w in xw:
+        w.wait()
+    gw1 = _wgrad(w1, dpre.view(c * world * R, 2 * F), xt.view(c * world * R, H), gaf)
+    for w in rs:
+        w.wait()
+    return dx, gw1, gw2
 
 
 def _weight_t_always(weight):
