@@ -452,13 +452,17 @@ void opt_prep(const at::Tensor& norm_sq, const c10::optional<at::Tensor>& inv_sc
 // ---------------------------------------------------------------- attention
 // Diagnostics: a uint64 buffer of 8 stamps per attention workgroup, attached
 // to every following launch until cleared (scripts/fa_stamps.py).
-static unsigned long long* g_fa_stamps = nullptr;
+// The buffer is kept referenced while attached (no use-after-free) and its
+// length travels with the pointer: a workgroup whose 8 stamps would not fit
+// writes none.
+static at::Tensor g_fa_stamps_buf;
 void fa_set_stamps(const c10::optional<at::Tensor>& buf) {
   if (buf.has_value() && buf->defined()) {
-    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "stamps: int64 buffer");
-    g_fa_stamps = reinterpret_cast<unsigned long long*>(buf->data_ptr<int64_t>());
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous() && buf->is_cuda(),
+                "stamps: contiguous int64 device buffer");
+    g_fa_stamps_buf = *buf;
   } else {
-    g_fa_stamps = nullptr;
+    g_fa_stamps_buf = at::Tensor();
   }
 }
 
@@ -506,7 +510,10 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   p.o_sb = os[0]; p.o_ss = os[1]; p.o_sh = os[2];
   p.causal = causal ? 1 : 0;
   p.scale = (float)scale;
-  p.stamps = g_fa_stamps;
+  if (g_fa_stamps_buf.defined()) {
+    p.stamps = reinterpret_cast<unsigned long long*>(g_fa_stamps_buf.data_ptr<int64_t>());
+    p.stamps_n = g_fa_stamps_buf.numel();
+  }
   return p;
 }
 

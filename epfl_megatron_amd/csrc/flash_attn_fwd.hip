@@ -273,7 +273,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   if (p.stamps) {  // diagnostics (scripts/fa_stamps.py)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores done
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && (int64_t)lin * 8 + 8 <= p.stamps_n) {
       unsigned long long* so = p.stamps + (int64_t)lin * 8;
       so[0] = st0; so[1] = st1; so[2] = st2; so[3] = fa::wall_stamp();
       so[4] = __smid(); so[5] = fa::xcc_id();

@@ -127,6 +127,7 @@ struct AttnParams {
   // Diagnostics only (null in production): per-workgroup s_memrealtime
   // stamps [entry, prologue done, loop done, exit, cu, xcc, 0, 0] (fa_set_stamps).
   unsigned long long* stamps;
+  int64_t stamps_n;  // elements of the stamps buffer
 };
 struct AttnBwdParams {
   AttnParams f;
