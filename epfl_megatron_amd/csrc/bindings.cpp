@@ -1033,6 +1033,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.def("wgrad_set_variant", &ema::wgrad_set_variant);
+  m.def("gemm_nt_ablation", [](const at::Tensor& a, const at::Tensor& b, at::Tensor c, int64_t mode) {
+    TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                    c.scalar_type() == at::kBFloat16 && a.is_contiguous() && b.is_contiguous() &&
+                    c.is_contiguous() && a.size(1) == b.size(1) && c.size(0) == a.size(0) &&
+                    c.size(1) == b.size(0) && a.size(1) % 64 == 0 && a.size(1) >= 128 &&
+                    b.size(0) % 8 == 0,
+                "gemm_nt_ablation: contiguous bf16 [M,K] x [N,K] -> [M,N], K % 64 == 0, K >= 128");
+    ema::gemm_nt_ablation(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.size(0), b.size(0), a.size(1),
+                          (int)mode, cur_stream());
+  });
   m.def("wgrad_plan", &wgrad_plan);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none(),
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},

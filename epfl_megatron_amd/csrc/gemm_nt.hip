@@ -734,8 +734,10 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
-template <typename T, int EPI, int ACT>
+template <typename T, int EPI, int ACT, int MODE = 0>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
+  // MODE (ablation builds, gemm_nt_ablation): 1 = no DMA in the K-loop,
+  // 2 = neither DMA nor fragment reads (MFMA + barriers + epilogue only)
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   const int lane = threadIdx.x & 63;
@@ -781,6 +783,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   };
   char* const ldsp = lds;
   auto dma = [&](int q, Rsrc r, uint32_t soff, int slot) {
+    if constexpr (MODE >= 1) return;
     const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
@@ -798,6 +801,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   }
   X8 set0[16], set1[16];
   auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
+    if constexpr (MODE >= 2) return;
     constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
     if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
     else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
@@ -978,6 +982,19 @@ void launch_nt(NtArgs& p, int kind, int dt, hipStream_t s) {
 }
 
 }  // namespace
+
+void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K,
+                      int mode, hipStream_t s) {
+  NtArgs p{a, b, c, nullptr, nullptr, K, K, N, 0, (int)M, (int)N, (int)K, 0, 0, 0, false,
+           RowMap{}, RowMap{}};
+  p.ntm = (p.M + TM - 1) / TM;
+  p.ntn = (p.N + TN - 1) / TN;
+  p.gm = group_m(p.ntm, p.ntn);
+  const int g = std::min(p.ntm * p.ntn, num_cus());
+  if (mode == 1) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 1>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 2) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 2>), dim3(g), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
+}
 
 void gemm_nt_set_variant(int v) { g_variant = (v == 8 || v == 4 || v == 6) ? v : 5; }
 
