@@ -41,6 +41,8 @@ namespace fa {
 namespace {
 
 
+typedef __attribute__((ext_vector_type(2))) float f2;
+
 template <typename T, int HD, bool CAUSAL, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnParams p) {
   typedef typename MT<T>::x8 x8;
@@ -193,36 +195,64 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
       });
       const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax) : (n0 + KT > p.sk);
       if (need_mask) {
+        // element i of s0 is key n0 + acc_row(i, h), of s1 that + 32: with
+        // rc = acc_row(i, 0) the tests are rc <= hi and rc >= lo, one compare
+        // and one select per element (lo only under a document mask)
+        int hi = p.sk - 1 - n0 - 4 * h;
+        if (CAUSAL) hi = min(hi, qrow + off - n0 - 4 * h);
+        if (CAUSAL && p.doc_start) {
+          const int lo = ds_row - n0 - 4 * h;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int k0 = n0 + acc_row(i, h), k1 = k0 + 32;
-          bool ok0 = k0 < p.sk, ok1 = k1 < p.sk;
-          if (CAUSAL) {
-            ok0 = ok0 && (k0 <= qrow + off) && (k0 >= ds_row);
-            ok1 = ok1 && (k1 <= qrow + off) && (k1 >= ds_row);
+          for (int i = 0; i < 16; ++i) {
+            const int rc = (i & 3) + 8 * (i >> 2);
+            if (rc > hi || rc < lo) s0[i] = -INFINITY;
+            if (rc + 32 > hi || rc + 32 < lo) s1[i] = -INFINITY;
           }
-          if (!ok0) s0[i] = -INFINITY;
-          if (!ok1) s1[i] = -INFINITY;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int rc = (i & 3) + 8 * (i >> 2);
+            if (rc > hi) s0[i] = -INFINITY;
+            if (rc + 32 > hi) s1[i] = -INFINITY;
+          }
         }
       }
-      float mt = -INFINITY;
+      // row max: 16 three-input max, the lane pair (l, l ^ 32) combined by one
+      // permlane32 swap (no LDS round trip)
+      float mt = fmaxf(s0[0], s1[0]);
 #pragma unroll
-      for (int i = 0; i < 16; i += 2)
-        mt = fmaxf(mt, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      for (int i = 1; i < 16; ++i) mt = fmaxf(fmaxf(mt, s0[i]), s1[i]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt),
+                                                         false, false);
+        mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+      }
       const float m_new = fmaxf(m_i, mt);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
-      float rs0 = 0.f, rs1 = 0.f;
+      // p = exp2(s * scale * log2e - m): packed fma for the argument, packed
+      // adds for the row sum
+      const f2 sc2 = {sl2, sl2}, mm2 = {-m_use, -m_use};
+      f2 rs2 = {0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sl2, -m_use));
-        s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sl2, -m_use));
-        rs0 += s0[i];
-        rs1 += s1[i];
+      for (int i = 0; i < 16; i += 2) {
+        f2 a = __builtin_elementwise_fma(f2{s0[i], s0[i + 1]}, sc2, mm2);
+        f2 b = __builtin_elementwise_fma(f2{s1[i], s1[i + 1]}, sc2, mm2);
+        a[0] = __builtin_amdgcn_exp2f(a[0]);
+        a[1] = __builtin_amdgcn_exp2f(a[1]);
+        b[0] = __builtin_amdgcn_exp2f(b[0]);
+        b[1] = __builtin_amdgcn_exp2f(b[1]);
+        s0[i] = a[0]; s0[i + 1] = a[1];
+        s1[i] = b[0]; s1[i + 1] = b[1];
+        rs2 += a;
+        rs2 += b;
       }
-      float rsum = rs0 + rs1;
-      rsum += __shfl_xor(rsum, 32, 64);
+      float rsum = rs2[0] + rs2[1];
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(rsum),
+                                                         __float_as_uint(rsum), false, false);
+        rsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+      }
       l_i = l_i * alpha + rsum;
       m_i = m_new;
       if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
