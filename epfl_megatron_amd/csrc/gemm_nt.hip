@@ -737,7 +737,9 @@ typedef __amdgpu_buffer_rsrc_t Rsrc;
 template <typename T, int EPI, int ACT, int MODE = 0>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   // MODE (ablation builds, gemm_nt_ablation): 1 = no DMA in the K-loop,
-  // 2 = neither DMA nor fragment reads (MFMA + barriers + epilogue only)
+  // 2 = neither DMA nor fragment reads (MFMA + barriers + epilogue only),
+  // 3 = DMA of the same (L2-resident) K-step every time, 4 = next-step wait
+  // 3 groups later, 5 = two DMA pieces per group
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   const int lane = threadIdx.x & 63;
@@ -783,7 +785,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   };
   char* const ldsp = lds;
   auto dma = [&](int q, Rsrc r, uint32_t soff, int slot) {
-    if constexpr (MODE >= 1) return;
+    if constexpr (MODE == 1 || MODE == 2) return;
     const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
@@ -801,7 +803,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   }
   X8 set0[16], set1[16];
   auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
-    if constexpr (MODE >= 2) return;
+    if constexpr (MODE == 2) return;
     constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
     if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
     else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
@@ -838,7 +840,10 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       // source of K-step t+2: this tile, else the next tile's step t+2-nt
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
-      const uint32_t soff = (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
+      const uint32_t soff = MODE == 3 ? 0u : (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
+      // schedule knobs of the ablation builds: WG = group of the step-t+1
+      // wait, DP = DMA pieces per group
+      constexpr int WG = MODE == 4 ? 26 : 23, DP = MODE == 5 ? 2 : 1;
       static_for<32>([&](auto g) {
         constexpr int GG = decltype(g)::value;
         if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
@@ -852,20 +857,26 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (GG >= 6 && GG < 14) dma(GG - 6, ra, soff, slot);
+        if constexpr (GG >= 6 && GG < 6 + 8 / DP)
+          static_for<DP>([&](auto e) { dma(DP * (GG - 6) + decltype(e)::value, ra, soff, slot); });
         if constexpr (GG >= 6 && GG < 10) {
           read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
           read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
         }
-        if constexpr (GG >= 12 && GG < 20) dma(8 + GG - 12, rb, soff, slot);
-        if constexpr (GG == 23) {
+        if constexpr (GG >= 12 && GG < 12 + 8 / DP)
+          static_for<DP>([&](auto e) { dma(8 + DP * (GG - 12) + decltype(e)::value, rb, soff, slot); });
+        if constexpr (GG == WG) {
           asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (GG >= 24) {
-          read_frag(set0, std::integral_constant<int, 2 * (GG - 24)>{}, K0{}, sn);
-          read_frag(set0, std::integral_constant<int, 2 * (GG - 24) + 1>{}, K0{}, sn);
+        if constexpr (GG > WG) {
+          // the 16 fragments of (t+1, k-half 0) spread over groups WG+1 .. 31
+          constexpr int NG = 31 - WG, Q = GG - WG - 1;
+          constexpr int F0 = 16 * Q / NG, F1 = 16 * (Q + 1) / NG;
+          static_for<F1 - F0>([&](auto e) {
+            read_frag(set0, std::integral_constant<int, F0 + decltype(e)::value>{}, K0{}, sn);
+          });
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -993,6 +1004,9 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   const int g = std::min(p.ntm * p.ntn, num_cus());
   if (mode == 1) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 1>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 2) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 2>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 3) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 3>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 4) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 4>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 5) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 5>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 

@@ -36,9 +36,12 @@ def main():
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
-        r = {k: [] for k in ("full", "no_dma", "mfma_only", "hipblaslt")}
+        modes = ((0, "full"), (1, "no_dma"), (2, "mfma_only"), (3, "dma_l2_resident"),
+                 (4, "late_wait"), (5, "dma_x2"))
+        r = {k: [] for _, k in modes}
+        r["hipblaslt"] = []
         for _ in range(5):
-            for mode, k in ((0, "full"), (1, "no_dma"), (2, "mfma_only")):
+            for mode, k in modes:
                 r[k].append(fl / _t(lambda: C.gemm_nt_ablation(a, b, c, mode)) / 1e12)
             r["hipblaslt"].append(fl / _t(lambda: torch.matmul(a, b.t(), out=c)) / 1e12)
         print(f"M={M} N={N} K={K}: " + "  ".join(

@@ -61,6 +61,22 @@ def main():
                   lambda x=x, w1=w1, pre=pre, y=y: C.gemm_nt_glu(x, w1, 0, pre, y, []),
                   lambda g=g, w1=w1, pre=pre, y=y: [C.gemm_nt_glu(g[j], w1, 0, pre, y, [R, c * R, j * R])
                                                     for j in range(c)]))
+    # piece-major GLU MLP (layers._sp_mlp_forward): every piece a plain product
+    # into its own contiguous buffer, no row remap
+    prep = torch.empty(c, tp * R, 2 * F, device=dev, dtype=dt)
+    yp = torch.empty(c, tp * R, F, device=dev, dtype=dt)
+    cases.append(("fc1+glu piece-major", 2.0 * M * 2 * F * H,
+                  lambda x=x, w1=w1, pre=pre, y=y: C.gemm_nt_glu(x, w1, 0, pre, y, []),
+                  lambda g=g, w1=w1, prep=prep, yp=yp: [C.gemm_nt_glu(g[j], w1, 0, prep[j], yp[j], [])
+                                                        for j in range(c)]))
+    w2 = r(H, F)
+    yfull = r(M, F)
+    o2 = torch.empty(M, H, device=dev, dtype=dt)
+    partp = torch.empty(c, tp * R, H, device=dev, dtype=dt)
+    cases.append(("fc2 piece-major", 2.0 * M * H * F,
+                  lambda y=yfull, w2=w2, o2=o2: C.gemm_nt(y, w2, o2),
+                  lambda y=yfull, w2=w2, partp=partp: [C.gemm_nt(y[j * tp * R:(j + 1) * tp * R], w2,
+                                                                 partp[j]) for j in range(c)]))
     # reduce-scatter side (attention out, fc2): the pieces read through a_map
     for name, k in (("o_proj", H // tp), ("fc2", F)):
         x, w = r(M, k), r(H, k)
