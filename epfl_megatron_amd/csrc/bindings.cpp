@@ -510,6 +510,8 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   p.o_sb = os[0]; p.o_ss = os[1]; p.o_sh = os[2];
   p.causal = causal ? 1 : 0;
   p.scale = (float)scale;
+  p.lse_sb = nq * sq;
+  p.lse_sh = sq;
   if (g_fa_stamps_buf.defined()) {
     p.stamps = reinterpret_cast<unsigned long long*>(g_fa_stamps_buf.data_ptr<int64_t>());
     p.stamps_n = g_fa_stamps_buf.numel();
@@ -566,6 +568,42 @@ void flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   auto p = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
   set_rope(p, rope_cos, rope_sin, rope_pos);
   set_docs(p, docs);
+  ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
+}
+
+// One ring-attention step (parallel/context.py): attention of q over this K/V
+// chunk, log-sum-exp combined in place with the running fp32 output o32
+// [b, sq, nq, hd] (any strides, head_dim contiguous) and lse [b, nq, sq] (any
+// batch / head strides, rows contiguous); merge = false stores instead.
+void flash_attn_fwd_merge(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                          at::Tensor o32, at::Tensor lse, int64_t b, int64_t sq, int64_t sk,
+                          int64_t nq, int64_t nkv, int64_t hd, std::vector<int64_t> qs,
+                          std::vector<int64_t> ks, std::vector<int64_t> vs, bool causal,
+                          double scale, bool merge) {
+  check_gpu(q, "q");
+  TORCH_CHECK(o32.scalar_type() == at::kFloat && o32.dim() == 4 && o32.size(0) == b &&
+                  o32.size(1) == sq && o32.size(2) == nq && o32.size(3) == hd && o32.stride(3) == 1 &&
+                  o32.stride(1) % 4 == 0 && o32.stride(2) % 4 == 0 && o32.stride(0) % 4 == 0 &&
+                  o32.data_ptr<float>() != nullptr && reinterpret_cast<uintptr_t>(o32.data_ptr()) % 16 == 0,
+              "flash_attn_fwd_merge: o32 fp32 [b, sq, nq, hd], head_dim contiguous, 16-B aligned");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.dim() == 3 && lse.size(0) == b &&
+                  lse.size(1) == nq && lse.size(2) == sq && lse.stride(2) == 1,
+              "flash_attn_fwd_merge: lse fp32 [b, nq, sq], rows contiguous");
+  TORCH_CHECK(o32.storage_offset() + (b - 1) * o32.stride(0) + (sq - 1) * o32.stride(1) +
+                      (nq - 1) * o32.stride(2) + hd <=
+                  (int64_t)(o32.storage().nbytes() / 4),
+              "o32 strides exceed storage");
+  // make_attn validates q / k / v; `out` is unused in this mode (o32 instead)
+  at::Tensor dummy = at::empty({b, sq, nq, hd}, q.options().device(q.device()));
+  std::vector<int64_t> os = {dummy.stride(0), dummy.stride(1), dummy.stride(2)};
+  auto p = make_attn(q, k, v, dummy, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  p.lse_sb = lse.stride(0);
+  p.lse_sh = lse.stride(1);
+  p.o32 = o32.data_ptr<float>();
+  p.o32_sb = o32.stride(0);
+  p.o32_ss = o32.stride(1);
+  p.o32_sh = o32.stride(2);
+  p.merge = merge ? 1 : 0;
   ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
 }
 
@@ -1083,6 +1121,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_fwd", &bias_dropout_add_fwd);
   m.def("bias_dropout_add_bwd", &bias_dropout_add_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_fwd_merge", &flash_attn_fwd_merge);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("fa_set_stamps", &fa_set_stamps);
   m.def("flash_decode", &flash_decode);

@@ -42,6 +42,9 @@ namespace ema {
 namespace fa {
 namespace {
 
+typedef __attribute__((ext_vector_type(2))) float f2;
+
+
 typedef __attribute__((ext_vector_type(4))) float f4;
 
 constexpr int BNK = 128;  // keys per dK/dV workgroup
@@ -297,27 +300,48 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
         const bool docs = CAUSAL && p.doc_start;
         const bool need_mask = (q0s + 32 > p.sq) || (kbase + 32 > p.sk) ||
                                (CAUSAL && (kbase + 31 > q0s + off)) || docs;
+        // P = exp2(S scale log2e - lse log2e), the argument by packed fma
+        const f2 sc2 = {sl2, sl2};
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -l24[i >> 2][i & 3]));
+        for (int i = 0; i < 16; i += 2) {
+          const f2 a = __builtin_elementwise_fma(
+              f2{sacc[i], sacc[i + 1]}, sc2, -f2{l24[i >> 2][i & 3], l24[i >> 2][(i & 3) + 1]});
+          sacc[i] = __builtin_amdgcn_exp2f(a[0]);
+          sacc[i + 1] = __builtin_amdgcn_exp2f(a[1]);
+        }
         if (need_mask) {
-          typedef __attribute__((ext_vector_type(4))) int i4;
-          i4 ds4[4] = {};
           if (docs) {
+            typedef __attribute__((ext_vector_type(4))) int i4;
+            i4 ds4[4];
             const int* dsl = reinterpret_cast<const int*>(cst + 2 * BQ2);
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg) ds4[rg] = *reinterpret_cast<const i4*>(dsl + 8 * rg);
-          }
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qr = q0s + acc_row(i, h);
-            const bool ok = (qr < p.sq) & (key < p.sk) &
-                            (!CAUSAL | ((key <= qr + off) & (key >= ds4[i >> 2][i & 3])));
-            sacc[i] = ok ? sacc[i] : 0.f;
+            for (int i = 0; i < 16; ++i) {
+              const int qr = q0s + acc_row(i, h);
+              const bool ok = (qr < p.sq) & (key < p.sk) & (key <= qr + off) &
+                              (key >= ds4[i >> 2][i & 3]);
+              sacc[i] = ok ? sacc[i] : 0.f;
+            }
+          } else {
+            // row rc = acc_row(i, 0) of the block is kept iff lo <= rc <= hi
+            int hi = p.sq - 1 - q0s - 4 * h;
+            if (key >= p.sk) hi = -1;
+            const int lo = CAUSAL ? key - off - q0s - 4 * h : -(1 << 30);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int rc = (i & 3) + 8 * (i >> 2);
+              if (rc > hi || rc < lo) sacc[i] = 0.f;
+            }
           }
         }
+        // dS = P (dP - delta): packed multiplies
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
+        for (int i = 0; i < 16; i += 2) {
+          const f2 d = f2{sacc[i], sacc[i + 1]} * f2{dpacc[i], dpacc[i + 1]};
+          dpacc[i] = d[0];
+          dpacc[i + 1] = d[1];
+        }
         lds_wait();  // the asm transposed reads above
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -580,15 +604,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
         const int kb = t * KT + sub * 32;
         f32x16 sacc, dpacc;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dpacc[i] = -dlt;
-#pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
           const int o = sub * 4 * RG + rowb[kk & 1] + 512 * (kk >> 1);
           const x8 ka = *reinterpret_cast<const x8*>(kl + o);
           const x8 va = *reinterpret_cast<const x8*>(vl + o);
           if (kk == 0) {
             sacc = mfma_vgpr0<T>(ka, qf[0]);
-            mfma_vgpr<T, 1>(dpacc, va, df[0]);
+            dpacc = mfma_vgpr0<T>(va, df[0]);
           } else {
             mfma_vgpr<T>(sacc, ka, qf[kk]);
             mfma_vgpr<T>(dpacc, va, df[kk]);
@@ -597,19 +619,40 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
         mfma_drain();
         const bool need_mask = (kb + 32 > p.sk) || (q0w + 32 > p.sq) ||
                                (CAUSAL && (kb + 31 > q0w + off || kb < ds_wmax));
+        const f2 sc2 = {sl2, sl2}, ml2 = {-lse2, -lse2}, nd2 = {-dlt, -dlt};
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          sacc[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], sl2, -lse2));
+        for (int i = 0; i < 16; i += 2) {
+          const f2 a = __builtin_elementwise_fma(f2{sacc[i], sacc[i + 1]}, sc2, ml2);
+          sacc[i] = __builtin_amdgcn_exp2f(a[0]);
+          sacc[i + 1] = __builtin_amdgcn_exp2f(a[1]);
+        }
         if (need_mask) {
+          // key rc = acc_row(i, 0) of the block is kept iff lo <= rc <= hi
+          int hi = p.sk - 1 - kb - 4 * h;
+          if (CAUSAL) hi = min(hi, qrow + off - kb - 4 * h);
+          if (qrow >= p.sq) hi = -1;
+          if (CAUSAL && p.doc_start) {
+            const int lo = ds_row - kb - 4 * h;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int kr = kb + acc_row(i, h);
-            const bool ok = (kr < p.sk) & (qrow < p.sq) & (!CAUSAL | ((kr <= qrow + off) & (kr >= ds_row)));
-            sacc[i] = ok ? sacc[i] : 0.f;
+            for (int i = 0; i < 16; ++i) {
+              const int rc = (i & 3) + 8 * (i >> 2);
+              if (rc > hi || rc < lo) sacc[i] = 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int rc = (i & 3) + 8 * (i >> 2);
+              if (rc > hi) sacc[i] = 0.f;
+            }
           }
         }
+        // dS = P (dP - delta): packed add and multiply
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] = sacc[i] * dpacc[i];
+        for (int i = 0; i < 16; i += 2) {
+          const f2 d = f2{sacc[i], sacc[i + 1]} * (f2{dpacc[i], dpacc[i + 1]} + nd2);
+          sacc[i] = d[0];
+          sacc[i + 1] = d[1];
+        }
         static_for<2>([&](auto sc) {
           const x8 sf = acc_frag<T>(sacc, decltype(sc)::value);
           static_for<DT>([&](auto dc) {

@@ -42,6 +42,7 @@ namespace {
 
 
 typedef __attribute__((ext_vector_type(2))) float f2;
+typedef __attribute__((ext_vector_type(4))) float f4;
 
 template <typename T, int HD, bool CAUSAL, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnParams p) {
@@ -284,20 +285,50 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   if (p.stamps) st2 = fa::wall_stamp();
   if (qrow < p.sq) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
-    T* O = (T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow * p.o_ss + (int64_t)head * p.o_sh;
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (T)(o[d][4 * rg + e] * inv);
-        *reinterpret_cast<x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
+    const float lse_j = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
+    float* lp = p.lse + (int64_t)b * p.lse_sb + (int64_t)head * p.lse_sh + qrow;
+    if (p.o32) {
+      // ring-attention step: combine with the running (O, lse) in place
+      float w_old = 0.f, w_new = inv, lse_new = lse_j;
+      if (p.merge) {
+        const float old = *lp;
+        const float mx = fmaxf(old, lse_j);
+        if (mx == -INFINITY) {
+          w_new = 0.f;
+        } else {
+          const float eo = __expf(old - mx), en = __expf(lse_j - mx), s = eo + en;
+          lse_new = mx + __logf(s);
+          w_old = eo / s;
+          w_new = inv * (en / s);
+        }
       }
-    }
-    if (h == 0) {
-      const float lse = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
-      p.lse[((int64_t)b * p.nq + head) * p.sq + qrow] = lse;
+      float* O32 = p.o32 + (int64_t)b * p.o32_sb + (int64_t)qrow * p.o32_ss + (int64_t)head * p.o32_sh;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          f4* dst = reinterpret_cast<f4*>(O32 + d * 32 + 8 * rg + 4 * h);
+          f4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = o[d][4 * rg + e] * w_new;
+          if (p.merge) v += *dst * w_old;
+          *dst = v;
+        }
+      }
+      if (h == 0) *lp = lse_new;
+    } else {
+      T* O = (T*)p.o + (int64_t)b * p.o_sb + (int64_t)qrow * p.o_ss + (int64_t)head * p.o_sh;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = (T)(o[d][4 * rg + e] * inv);
+          *reinterpret_cast<x4*>(O + d * 32 + 8 * rg + 4 * h) = w;
+        }
+      }
+      if (h == 0) *lp = lse_j;
     }
   }
   if (p.stamps) {  // diagnostics (scripts/fa_stamps.py)

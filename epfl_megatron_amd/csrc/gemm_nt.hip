@@ -739,7 +739,8 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   // MODE (ablation builds, gemm_nt_ablation): 1 = no DMA in the K-loop,
   // 2 = neither DMA nor fragment reads (MFMA + barriers + epilogue only),
   // 3 = DMA of the same (L2-resident) K-step every time, 4 = next-step wait
-  // 3 groups later, 5 = two DMA pieces per group
+  // 3 groups later, 5 = two DMA pieces per group, 7 = the same global reads
+  // into registers (no LDS write), 9 = A pieces only
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   const int lane = threadIdx.x & 63;
@@ -786,6 +787,12 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   char* const ldsp = lds;
   auto dma = [&](int q, Rsrc r, uint32_t soff, int slot) {
     if constexpr (MODE == 1 || MODE == 2) return;
+    if constexpr (MODE == 9) { if (q >= 8) return; }  // A pieces only
+    if constexpr (MODE == 7) {  // same global reads into a scratch VGPR: no LDS write
+      uint4 d;
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(off[q]), "s"(r), "s"(soff) : "memory");
+      return;
+    }
     const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
@@ -1007,6 +1014,8 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else if (mode == 3) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 3>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 4) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 4>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 5) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 5>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 7) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 7>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 9) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 9>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 

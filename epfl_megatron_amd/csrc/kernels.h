@@ -128,6 +128,16 @@ struct AttnParams {
   // stamps [entry, prologue done, loop done, exit, cu, xcc, 0, 0] (fa_set_stamps).
   unsigned long long* stamps;
   int64_t stamps_n;  // elements of the stamps buffer
+  // lse element strides (batch, head); the row stride is 1
+  int64_t lse_sb, lse_sh;
+  // Forward only, context-parallel ring attention (parallel/context.py): a
+  // running fp32 output o32 (element strides o32_sb / ss / sh, head_dim
+  // contiguous) and the running lse.  merge = 0: store this pair's normalised
+  // output and lse there; merge = 1: log-sum-exp combine them with what is
+  // there.  p.o (16-bit) is not written when o32 is set.
+  float* o32;
+  int64_t o32_sb, o32_ss, o32_sh;
+  int merge;
 };
 struct AttnBwdParams {
   AttnParams f;
