@@ -471,7 +471,7 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
                           int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
                           const std::vector<int64_t>& qs, const std::vector<int64_t>& ks,
                           const std::vector<int64_t>& vs, const std::vector<int64_t>& os,
-                          bool causal, double scale) {
+                          bool causal, double scale, bool lse_view = false) {
   TORCH_CHECK(qs.size() == 4 && ks.size() == 3 && vs.size() == 3 && os.size() == 3, "bad strides");
   TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type() &&
               q.scalar_type() == out.scalar_type(), "q/k/v/out dtype mismatch");
@@ -479,7 +479,8 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
               "with head_dim 64 or 128 (got ", hd, ")");
   TORCH_CHECK(nkv > 0 && nq % nkv == 0, "nq must be a multiple of nkv");
   TORCH_CHECK(sq > 0 && sk > 0 && b > 0, "empty attention");
-  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == b * nq * sq && lse.is_contiguous(),
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == b * nq * sq &&
+                  (lse_view || lse.is_contiguous()),
               "lse must be fp32 [b, nq, sq]");
   for (int64_t s : qs) TORCH_CHECK(s % 8 == 0, "q strides must keep 16-byte alignment");
   for (int64_t s : ks) TORCH_CHECK(s % 8 == 0, "k strides must keep 16-byte alignment");
@@ -593,10 +594,12 @@ void flash_attn_fwd_merge(const at::Tensor& q, const at::Tensor& k, const at::Te
                       (nq - 1) * o32.stride(2) + hd <=
                   (int64_t)(o32.storage().nbytes() / 4),
               "o32 strides exceed storage");
-  // make_attn validates q / k / v; `out` is unused in this mode (o32 instead)
-  at::Tensor dummy = at::empty({b, sq, nq, hd}, q.options().device(q.device()));
-  std::vector<int64_t> os = {dummy.stride(0), dummy.stride(1), dummy.stride(2)};
-  auto p = make_attn(q, k, v, dummy, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
+  // make_attn validates q / k / v; no 16-bit output is written in this mode
+  // (q stands in for `out` in the validation only)
+  TORCH_CHECK(q.dim() == 4 && q.size(0) == b && q.size(1) == sq, "flash_attn_fwd_merge: q [b, sq, ...]");
+  std::vector<int64_t> os = {qs[0], qs[1], qs[3]};
+  auto p = make_attn(q, k, v, q, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale, true);
+  p.o = nullptr;
   p.lse_sb = lse.stride(0);
   p.lse_sh = lse.stride(1);
   p.o32 = o32.data_ptr<float>();

@@ -115,6 +115,19 @@ def _pair_bwd(q, k, v, o, lse, do, causal, scale):
     return dq.float(), dk.float(), dv.float()
 
 
+def _pair_fwd_into(q, k, v, o32, lse, causal, scale, merge):
+    """GPU: one pair's attention log-sum-exp combined IN the kernel epilogue with
+    the running fp32 output ``o32`` [b, s, nq, d] and ``lse`` [b, nq, s] (views
+    allowed): no O_j / LSE_j tensors and no separate merge kernels."""
+    from ..ops._ext import ext
+    b, sq, nq, d = q.shape
+    sk, nkv = k.shape[1], k.shape[2]
+    r = nq // nkv
+    ext().flash_attn_fwd_merge(q, k, v, o32, lse, b, sq, sk, nq, nkv, d, _strides(q, r),
+                               _strides(k, 1)[:3], _strides(v, 1)[:3], bool(causal), float(scale),
+                               bool(merge))
+
+
 def _merge(o, lse, o_j, lse_j):
     """Log-sum-exp combine of two partial attentions ([b, s, n, d], [b, n, s])."""
     if o is None:
@@ -178,6 +191,12 @@ class _RingAttnFn(torch.autograd.Function):
         W, r = ring.world, ring.rank
         h = q.shape[1] // 2
         o = lse = None
+        fused = q.is_cuda
+        if fused:  # running output / lse, merged by the kernels in place
+            b, s, nq, d = q.shape
+            o = torch.empty(b, s, nq, d, dtype=torch.float32, device=q.device)
+            lse = torch.empty(b, nq, s, dtype=torch.float32, device=q.device)
+        started = False
         kv = [k.contiguous(), v.contiguous()]
         for i in range(W):
             j = (r - i) % W
@@ -187,14 +206,21 @@ class _RingAttnFn(torch.autograd.Function):
             plan = _plan(j, r, causal, zigzag)
             if plan is not None:
                 qs, ks, c = plan
-                o_j, lse_j = _pair_fwd(_rows(q, qs), _rows(kv[0], ks), _rows(kv[1], ks), c,
-                                       scale)
-                if qs == "all":
-                    o, lse = _merge(o, lse, o_j, lse_j)
-                else:  # late query piece only (step 0 is the diagonal: o is set)
-                    o2, l2 = _merge(o[:, h:], lse[..., h:], o_j, lse_j)
-                    o = torch.cat([o[:, :h], o2], 1)
-                    lse = torch.cat([lse[..., :h], l2], -1)
+                if fused:
+                    # step 0 is the diagonal ("all" rows): it initialises o / lse
+                    _pair_fwd_into(_rows(q, qs), _rows(kv[0], ks), _rows(kv[1], ks),
+                                   _rows(o, qs), lse if qs == "all" else lse[..., h:], c, scale,
+                                   merge=started)
+                    started = True
+                else:
+                    o_j, lse_j = _pair_fwd(_rows(q, qs), _rows(kv[0], ks), _rows(kv[1], ks), c,
+                                           scale)
+                    if qs == "all":
+                        o, lse = _merge(o, lse, o_j, lse_j)
+                    else:  # late query piece only (step 0 is the diagonal: o is set)
+                        o2, l2 = _merge(o[:, h:], lse[..., h:], o_j, lse_j)
+                        o = torch.cat([o[:, :h], o2], 1)
+                        lse = torch.cat([lse[..., :h], l2], -1)
             if work is not None:
                 work.wait()
                 kv = recv
@@ -279,12 +305,23 @@ def ring_attention_simulated(qs, ks, vs, causal=True, softmax_scale=None, grad_o
     for r in range(W):
         h = qs[r].shape[1] // 2
         o = lse = None
+        fused = qs[r].is_cuda
+        if fused:
+            b, s, nq, d = qs[r].shape
+            o = torch.empty(b, s, nq, d, dtype=torch.float32, device=qs[r].device)
+            lse = torch.empty(b, nq, s, dtype=torch.float32, device=qs[r].device)
+        started = False
         for i in range(W):
             j = (r - i) % W
             plan = _plan(j, r, causal, zigzag)
             if plan is None:
                 continue
             q_, k_, c = plan
+            if fused:
+                _pair_fwd_into(_rows(qs[r], q_), _rows(ks[j], k_), _rows(vs[j], k_), _rows(o, q_),
+                               lse if q_ == "all" else lse[..., h:], c, scale, merge=started)
+                started = True
+                continue
             o_j, lse_j = _pair_fwd(_rows(qs[r], q_), _rows(ks[j], k_), _rows(vs[j], k_), c, scale)
             if q_ == "all":
                 o, lse = _merge(o, lse, o_j, lse_j)
