@@ -870,10 +870,14 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
           read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
           read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
         }
-        if constexpr (GG >= 12 && GG < 12 + 8 / DP)
-          static_for<DP>([&](auto e) { dma(8 + DP * (GG - 12) + decltype(e)::value, rb, soff, slot); });
+        // B pieces: G 12.. (default) or, MODE 10, after the step-t+1 wait (G 24..31),
+        // which caps this wave's VMEM in flight at 16 instead of 32
+        constexpr int BG = MODE == 10 ? WG + 1 : 12;
+        if constexpr (GG >= BG && GG < BG + 8 / DP)
+          static_for<DP>([&](auto e) { dma(8 + DP * (GG - BG) + decltype(e)::value, rb, soff, slot); });
         if constexpr (GG == WG) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          if constexpr (MODE == 10) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
@@ -1016,6 +1020,7 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else if (mode == 5) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 5>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 7) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 7>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 9) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 9>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 10) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 10>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 

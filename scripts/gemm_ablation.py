@@ -37,7 +37,7 @@ def main():
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
         modes = ((0, "full"), (1, "no_dma"), (2, "mfma_only"), (3, "dma_l2_resident"),
-                 (7, "vgpr_loads"), (9, "dma_A_only"))
+                 (7, "vgpr_loads"), (9, "dma_A_only"), (10, "B_after_wait"))
         r = {k: [] for _, k in modes}
         r["hipblaslt"] = []
         for _ in range(5):
