@@ -734,6 +734,101 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
+// Two accumulator fragments (cols 16 j + 4 q' and 16 (j+1) + 4 q' of one row on
+// lane group q' = lane >> 4), packed to 16 bits, become 8 CONSECUTIVE columns
+// 8 q' .. 8 q' + 7 of the fragment pair on every lane: one permlane32 and one
+// permlane16 swap per dword.
+__device__ __forceinline__ uint4 pair_to_row8(uint2 x, uint2 y) {
+  auto s0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+  auto s1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+  auto t0 = __builtin_amdgcn_permlane16_swap(s0[0], s0[1], false, false);
+  auto t1 = __builtin_amdgcn_permlane16_swap(s1[0], s1[1], false, false);
+  return make_uint4(t0[0], t1[0], t0[1], t1[1]);
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 unpack4(uint2 v) {
+  typename fa::MT<T>::x4 h = *reinterpret_cast<typename fa::MT<T>::x4*>(&v);
+  return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+
+// Register epilogue of the persistent kernel: the wave's 128 x 128 accumulator
+// tile at (gm0, gn0).  STORE: C; GLU: gn0 is the first f, fragments 0-3 are up,
+// 4-7 the gate of the same f (pre-activation and y = up * act(gate) stored);
+// DGLU: d(pre) from dAct (rounded to T) and the saved pre-activation.
+template <typename T, int EPI, int ACT>
+__device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc)[8][8], int lane,
+                                              int64_t gm0, int64_t gn0) {
+  typedef V16<T> V;
+  const int M = p.M, N = p.N, q = lane >> 4;
+#pragma unroll
+  for (int ii = 0; ii < 8; ++ii) {
+    const int64_t row = gm0 + 16 * ii + (lane & 15);
+    const bool rok = row < M;
+    if constexpr (EPI == EPI_STORE) {
+      T* c = reinterpret_cast<T*>(p.c);
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const uint4 v = pair_to_row8(pack4<T>(acc[ii][2 * jp]), pack4<T>(acc[ii][2 * jp + 1]));
+        const int64_t col = gn0 + 32 * jp + 8 * q;
+        if (rok && col < N) *reinterpret_cast<uint4*>(c + row * p.ldc + col) = v;
+      }
+    } else if constexpr (EPI == EPI_GLU) {
+      T* pre = reinterpret_cast<T*>(p.c);
+      T* y = reinterpret_cast<T*>(p.y);
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        uint2 u[2], g[2], yy[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          u[e] = pack4<T>(acc[ii][2 * jp + e]);
+          g[e] = pack4<T>(acc[ii][4 + 2 * jp + e]);
+          const f32x4 uf = unpack4<T>(u[e]), gf = unpack4<T>(g[e]);
+          yy[e] = pack4<T>(f32x4{uf[0] * act<ACT>(gf[0]), uf[1] * act<ACT>(gf[1]),
+                                 uf[2] * act<ACT>(gf[2]), uf[3] * act<ACT>(gf[3])});
+        }
+        const uint4 vu = pair_to_row8(u[0], u[1]), vg = pair_to_row8(g[0], g[1]);
+        const uint4 vy = pair_to_row8(yy[0], yy[1]);
+        const int64_t f = gn0 + 32 * jp + 8 * q;
+        if (rok && f < N) {
+          *reinterpret_cast<uint4*>(pre + row * p.ldc + f) = vu;
+          *reinterpret_cast<uint4*>(pre + row * p.ldc + N + f) = vg;
+          *reinterpret_cast<uint4*>(y + row * p.ldy + f) = vy;
+        }
+      }
+    } else {
+      const T* pre = reinterpret_cast<const T*>(p.pre);
+      T* d = reinterpret_cast<T*>(p.c);
+      const int64_t rr = rok ? row : M - 1;
+      V x1[4], x2[4];
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        int64_t f = gn0 + 32 * jp + 8 * q;
+        f = f < N ? f : 0;
+        x1[jp] = ld16(pre + rr * p.ldc + f);
+        x2[jp] = ld16(pre + rr * p.ldc + N + f);
+      }
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const uint4 gv = pair_to_row8(pack4<T>(acc[ii][2 * jp]), pack4<T>(acc[ii][2 * jp + 1]));
+        const V g = *reinterpret_cast<const V*>(&gv);
+        V da, dg;
+#pragma unroll
+        for (int e = 0; e < V::N; ++e) {
+          const float gf = to_f(g.v[e]), xg = to_f(x2[jp].v[e]);
+          da.v[e] = from_f<T>(gf * act<ACT>(xg));
+          dg.v[e] = from_f<T>(gf * to_f(x1[jp].v[e]) * dact<ACT>(xg));
+        }
+        const int64_t f = gn0 + 32 * jp + 8 * q;
+        if (rok && f < N) {
+          st16(d + row * p.ldc + f, da);
+          st16(d + row * p.ldc + N + f, dg);
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int EPI, int ACT, int MODE = 0>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   // MODE (ablation builds, gemm_nt_ablation): 1 = no DMA in the K-loop,
@@ -760,15 +855,22 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
     const int tr = 8 * (8 * wave + i) + (lane >> 3);
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
     off[i] = (uint32_t)(tr * p.lda + 8 * c) * (uint32_t)sizeof(T);
-    off[8 + i] = (uint32_t)(tr * p.ldb + 8 * c) * (uint32_t)sizeof(T);
+    int br = tr;  // B row relative to the tile's first row n0
+    if constexpr (EPI == EPI_GLU) {
+      // per 128-row wave band: 64 up rows f then the 64 gate rows F + f
+      const int band = tr >> 7, q = tr & 127;
+      br = q < 64 ? 64 * band + q : N + 64 * band + (q - 64);
+    }
+    off[8 + i] = (uint32_t)(br * p.ldb + 8 * c) * (uint32_t)sizeof(T);
   }
-  // tile i of this workgroup -> (m0, n0)
+  // tile i of this workgroup -> (m0, n0): n0 = first output column, or first
+  // f (EPI_GLU: 128 per tile)
   auto tile_org = [&](int i, int64_t& m0, int64_t& n0) {
     const int base = i * G, rem = min(G, ntiles - base);
     const int lin = base + xcd_remap(bid, rem);
     const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
     m0 = (int64_t)tt.x * TM;
-    n0 = (int64_t)tt.y * TN;
+    n0 = (int64_t)tt.y * (EPI == EPI_GLU ? TN / 2 : TN);
   };
   // descriptors of tile i (size 0 past the last tile: every load is dropped)
   auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
@@ -777,7 +879,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
     if (i < nmine) {
       tile_org(i, m0, n0);
       na = (int64_t)(M - m0) * p.lda * (int64_t)sizeof(T);
-      nb = (int64_t)(N - n0) * p.ldb * (int64_t)sizeof(T);
+      nb = (int64_t)((EPI == EPI_GLU ? 2 * (int64_t)N : N) - n0) * p.ldb * (int64_t)sizeof(T);
     }
     const char* a = reinterpret_cast<const char*>(p.a) + m0 * p.lda * (int64_t)sizeof(T);
     const char* b = reinterpret_cast<const char*>(p.b) + n0 * p.ldb * (int64_t)sizeof(T);
@@ -848,9 +950,23 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
       const uint32_t soff = MODE == 3 ? 0u : (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
-      // schedule knobs of the ablation builds: WG = group of the step-t+1
-      // wait, DP = DMA pieces per group
-      constexpr int WG = MODE == 4 ? 26 : 23, DP = MODE == 5 ? 2 : 1;
+      // Schedule (per K-step, groups of 4 MFMAs): A DMA piece k at group
+      // GA + SA k, B piece k at GB + SB k, the step-t+1 wait at group WG with
+      // vmcnt = the pieces issued up to and including WG.  The production
+      // schedule (MODE 0) spreads the 16 pieces over groups 6-27: the per-CU
+      // L2 -> LDS fill path saturates when the 4 waves' pieces come in one
+      // burst (ablation modes: profiles/r4f_gemm_ablation.txt).
+      constexpr int WG = MODE == 4 ? 26 : MODE == 13 ? 25 : 23;
+      constexpr bool SPREAD = MODE == 0 || MODE == 11 || MODE == 13;
+      constexpr int GA = 6, SA = SPREAD ? 2 : MODE == 12 ? 3 : MODE == 5 ? 0 : 1;
+      constexpr int GB = SPREAD ? 13 : MODE == 12 ? 12 : MODE == 10 ? WG + 1 : 12;
+      constexpr int SB = SPREAD || MODE == 12 ? 2 : MODE == 5 ? 0 : 1;
+      auto n_upto = [](int g0, int st, int g) constexpr {
+        int n = 0;
+        for (int k = 0; k < 8; ++k) n += (st == 0 ? g0 + k / 2 : g0 + st * k) <= g;
+        return n;
+      };
+      constexpr int VM = n_upto(GA, SA, WG) + n_upto(GB, SB, WG);
       static_for<32>([&](auto g) {
         constexpr int GG = decltype(g)::value;
         if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
@@ -864,20 +980,20 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (GG >= 6 && GG < 6 + 8 / DP)
-          static_for<DP>([&](auto e) { dma(DP * (GG - 6) + decltype(e)::value, ra, soff, slot); });
+        // (SA / SB == 0: two pieces per group)
+        static_for<8>([&](auto kk) {
+          constexpr int K_ = decltype(kk)::value;
+          constexpr int ga = SA == 0 ? GA + K_ / 2 : GA + SA * K_;
+          constexpr int gb = SB == 0 ? GB + K_ / 2 : GB + SB * K_;
+          if constexpr (ga == GG) dma(K_, ra, soff, slot);
+          if constexpr (gb == GG) dma(8 + K_, rb, soff, slot);
+        });
         if constexpr (GG >= 6 && GG < 10) {
           read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
           read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
         }
-        // B pieces: G 12.. (default) or, MODE 10, after the step-t+1 wait (G 24..31),
-        // which caps this wave's VMEM in flight at 16 instead of 32
-        constexpr int BG = MODE == 10 ? WG + 1 : 12;
-        if constexpr (GG >= BG && GG < BG + 8 / DP)
-          static_for<DP>([&](auto e) { dma(8 + DP * (GG - BG) + decltype(e)::value, rb, soff, slot); });
         if constexpr (GG == WG) {
-          if constexpr (MODE == 10) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
@@ -902,24 +1018,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
     fa::mfma_drain();
     int64_t m0, n0;
     tile_org(i, m0, n0);
-    T* c = reinterpret_cast<T*>(p.c);
-    const int q = lane >> 4;
-    const int64_t col0 = n0 + 128 * wn + 8 * q;
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-      const int64_t row = m0 + 128 * wm + 16 * ii + (lane & 15);
-#pragma unroll
-      for (int jp = 0; jp < 4; ++jp) {
-        uint2 x = pack4<T>(acc[ii][2 * jp]), y = pack4<T>(acc[ii][2 * jp + 1]);
-        auto s0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
-        auto s1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
-        auto t0 = __builtin_amdgcn_permlane16_swap(s0[0], s0[1], false, false);
-        auto t1 = __builtin_amdgcn_permlane16_swap(s1[0], s1[1], false, false);
-        const int64_t col = col0 + 32 * jp;
-        if (row < M && col < N)
-          *reinterpret_cast<uint4*>(c + row * p.ldc + col) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
-      }
-    }
+    epilogue_regs<T, EPI, ACT>(p, acc, lane, m0 + 128 * wm, n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
     par ^= nt & 1;
     ra_c = ra_n;
     rb_c = rb_n;
@@ -967,10 +1066,14 @@ int num_cus() {
 template <typename T, int EPI, int ACT>
 void launch_one(const NtArgs& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.ntm * p.ntn));
-  if constexpr (EPI == EPI_STORE) {
+  // (the GeGLU backward's erf-based derivative would spill the accumulators:
+  // that form stays on the one-shot kernel)
+  if constexpr (!(EPI == EPI_DGLU && ACT == 1)) {
     const int64_t lim = (int64_t)1 << 31;
-    if (g_variant == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 && p.am.rows == 0 && p.cm.rows == 0 &&
-        (int64_t)p.M * p.lda * 2 < lim && (int64_t)p.N * p.ldb * 2 < lim) {
+    const int64_t brows = EPI == EPI_GLU ? 2 * (int64_t)p.N : p.N;
+    if (g_variant == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 &&
+        p.am.rows == 0 && p.cm.rows == 0 &&
+        (int64_t)p.M * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
       const int g = std::min(p.ntm * p.ntn, num_cus());
       hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, p);
       return;
@@ -1021,6 +1124,10 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else if (mode == 7) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 7>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 9) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 9>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 10) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 10>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 11) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 11>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 12) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 12>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 13) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 13>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 14) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 14>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 

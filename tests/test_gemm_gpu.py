@@ -143,6 +143,32 @@ def test_gemm_nt_dglu_backward(M, F, K, kind):
     assert _rel_err(dpre, p32.grad) < 1.5e-2
 
 
+@pytest.mark.parametrize("M,F,K", [(256, 128, 128), (300, 200, 192), (1024, 1376, 512),
+                                   (4096, 2752, 1024)])
+@pytest.mark.parametrize("kind", ["swiglu", "reglu"])
+def test_gemm_nt_glu_persistent_matches_oneshot(M, F, K, kind):
+    """The persistent kernel's register epilogues (variant 6) give the one-shot
+    kernel's GLU forward and backward outputs exactly (same rounding points)."""
+    torch.manual_seed(5)
+    kinds = {"swiglu": 0, "reglu": 2}
+    C = _ext()
+    x = _rand(M, K)
+    w1 = _rand(2 * F, K, scale=K ** -0.5)
+    pre = _rand(M, 2 * F)
+    dy = _rand(M, K)
+    w2t = _rand(F, K, scale=F ** -0.5)
+    outs = {}
+    for v in (5, 6):
+        C.gemm_nt_set_variant(v)
+        try:
+            outs[v] = (*C.gemm_nt_glu(x, w1, kinds[kind]), C.gemm_nt_dglu(dy, w2t, pre, kinds[kind]))
+        finally:
+            C.gemm_nt_set_variant(0)
+    for a, b in zip(outs[5], outs[6]):
+        assert torch.equal(a, b)
+    assert _rel_err(outs[6][0], x.float() @ w1.float().t()) < 8e-3
+
+
 def test_gemm_nt_matches_unfused_path():
     """Fused fc1 + fc2-dgrad == hipBLASLt matmul + the elementwise GLU kernels."""
     from epfl_megatron_amd.ops.activations import glu
