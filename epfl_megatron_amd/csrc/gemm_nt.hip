@@ -852,7 +852,8 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   uint32_t off[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int tr = 8 * (8 * wave + i) + (lane >> 3);
+    const int pb = MODE == 15 ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
+    const int tr = 8 * pb + (lane >> 3);
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
     off[i] = (uint32_t)(tr * p.lda + 8 * c) * (uint32_t)sizeof(T);
     int br = tr;  // B row relative to the tile's first row n0
@@ -895,7 +896,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(off[q]), "s"(r), "s"(soff) : "memory");
       return;
     }
-    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (8 * wave + (q & 7)) * 1024;
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (MODE == 15 ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
   };
@@ -957,7 +958,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       // L2 -> LDS fill path saturates when the 4 waves' pieces come in one
       // burst (ablation modes: profiles/r4f_gemm_ablation.txt).
       constexpr int WG = MODE == 4 ? 26 : MODE == 13 ? 25 : 23;
-      constexpr bool SPREAD = MODE == 0 || MODE == 11 || MODE == 13;
+      constexpr bool SPREAD = MODE == 0 || MODE == 11 || MODE == 13 || MODE == 15;
       constexpr int GA = 6, SA = SPREAD ? 2 : MODE == 12 ? 3 : MODE == 5 ? 0 : 1;
       constexpr int GB = SPREAD ? 13 : MODE == 12 ? 12 : MODE == 10 ? WG + 1 : 12;
       constexpr int SB = SPREAD || MODE == 12 ? 2 : MODE == 5 ? 0 : 1;
@@ -1128,6 +1129,7 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else if (mode == 12) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 12>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 13) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 13>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 14) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 14>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 15) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 15>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 
