@@ -852,7 +852,8 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   uint32_t off[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int pb = MODE == 15 ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
+    const int pb = (MODE == 0 || MODE == 15) ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
+    // (piece i of the 4 waves = 32 consecutive rows: +1-3 %, profiles/r4h_gemm_ablation.txt)
     const int tr = 8 * pb + (lane >> 3);
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
     off[i] = (uint32_t)(tr * p.lda + 8 * c) * (uint32_t)sizeof(T);
@@ -896,7 +897,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(off[q]), "s"(r), "s"(soff) : "memory");
       return;
     }
-    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (MODE == 15 ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + ((MODE == 0 || MODE == 15) ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
   };
@@ -1045,12 +1046,21 @@ int group_m(int ntm, int ntn) {
     default: { constexpr int A_ = 3; __VA_ARGS__; break; }    \
   }
 
-// Kernel variant: 4 (one wave per SIMD, default) or 8 (ping-pong); the
-// EMA_GEMM_NT environment variable sets the initial value, gemm_nt_set_variant
-// switches it at run time (A/B in one process).
-int g_variant = [] {
+// Kernel variant per epilogue: 5 (one-shot early-refill 4-wave), 6 (persistent
+// 4-wave, register epilogue), 4 (one-shot, one refill point), 8 (8-wave
+// ping-pong).  Defaults from interleaved same-box A/B on the 7B shapes
+// (profiles/r4g_gemm_nt_bench.txt): fc2 dgrad + dGLU on 6 (1.07x hipBLASLt +
+// glu kernel vs 1.05x on 5), fc1 + GLU on 5 (1.01x vs 0.97x), plain products
+// on 5 (they run on hipBLASLt in-model unless a row map needs this kernel).
+// EMA_GEMM_NT=<v> or gemm_nt_set_variant(v) forces one variant everywhere
+// (A/B in one process); gemm_nt_set_variant(0) restores the defaults.
+int g_var[3] = {5, 5, 6};  // [EPI_STORE, EPI_GLU, EPI_DGLU]
+int parse_variant(int v) { return (v == 4 || v == 5 || v == 6 || v == 8) ? v : 0; }
+const int g_env_variant = [] {
   const char* e = getenv("EMA_GEMM_NT");
-  return e ? (e[0] == '8' ? 8 : e[0] == '4' ? 4 : e[0] == '6' ? 6 : 5) : 5;
+  const int v = e ? parse_variant(atoi(e)) : 0;
+  if (v) g_var[0] = g_var[1] = g_var[2] = v;
+  return v;
 }();
 
 int num_cus() {
@@ -1072,7 +1082,7 @@ void launch_one(const NtArgs& p, hipStream_t s) {
   if constexpr (!(EPI == EPI_DGLU && ACT == 1)) {
     const int64_t lim = (int64_t)1 << 31;
     const int64_t brows = EPI == EPI_GLU ? 2 * (int64_t)p.N : p.N;
-    if (g_variant == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 &&
+    if (g_var[EPI] == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 &&
         p.am.rows == 0 && p.cm.rows == 0 &&
         (int64_t)p.M * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
       const int g = std::min(p.ntm * p.ntn, num_cus());
@@ -1080,8 +1090,8 @@ void launch_one(const NtArgs& p, hipStream_t s) {
       return;
     }
   }
-  const bool w4 = g_variant != 8 && p.K % BK2 == 0 && p.wave4_ok;
-  if (w4 && g_variant == 5) hipLaunchKernelGGL((gemm_nt5_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
+  const bool w4 = g_var[EPI] != 8 && p.K % BK2 == 0 && p.wave4_ok;
+  if (w4 && g_var[EPI] != 4) hipLaunchKernelGGL((gemm_nt5_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
   else if (w4) hipLaunchKernelGGL((gemm_nt4_k<T, EPI, ACT>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt_k<T, EPI, ACT>), grid, dim3(512), 0, s, p);
 }
@@ -1133,7 +1143,14 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 
-void gemm_nt_set_variant(int v) { g_variant = (v == 8 || v == 4 || v == 6) ? v : 5; }
+void gemm_nt_set_variant(int v) {
+  v = parse_variant(v);
+  if (v) {
+    g_var[0] = g_var[1] = g_var[2] = v;
+  } else {
+    g_var[0] = 5; g_var[1] = 5; g_var[2] = 6;
+  }
+}
 
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
   return M > 0 && N > 0 && K > 0 && K % BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
