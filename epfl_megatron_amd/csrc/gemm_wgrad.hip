@@ -622,14 +622,16 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (GG >= 6 && GG < 14) dmaq(GG - 6, ra, rb, s2, slot);
+        // DMA pieces spread over the K-step (dY at groups 6, 8, .., 20; X at
+        // 13, 15, .., 27): the per-CU fill path stalls on bursts (gemm_nt.hip)
+        if constexpr (GG >= 6 && GG <= 20 && (GG - 6) % 2 == 0) dmaq((GG - 6) / 2, ra, rb, s2, slot);
         if constexpr (GG >= 6 && GG < 10) {
           read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
           read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
         }
-        if constexpr (GG >= 12 && GG < 20) dmaq(8 + GG - 12, ra, rb, s2, slot);
+        if constexpr (GG >= 13 && GG <= 27 && (GG - 13) % 2 == 0) dmaq(8 + (GG - 13) / 2, ra, rb, s2, slot);
         if constexpr (GG == 23) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // 8 dY + 6 X pieces of step t+2 may fly
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
