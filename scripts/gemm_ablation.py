@@ -36,7 +36,7 @@ def main():
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
-        modes = ((0, "spread"), (15, "spread_rows_interleaved"), (1, "no_dma"))
+        modes = ((0, "spread+interleaved"), (16, "one_mfma_slots"), (1, "no_dma"))
         r = {k: [] for _, k in modes}
         r["hipblaslt"] = []
         for _ in range(5):
