@@ -852,7 +852,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   uint32_t off[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int pb = (MODE == 0 || MODE == 15 || MODE == 16) ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
+    const int pb = (MODE == 0 || MODE >= 15) ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
     // (piece i of the 4 waves = 32 consecutive rows: +1-3 %, profiles/r4h_gemm_ablation.txt)
     const int tr = 8 * pb + (lane >> 3);
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
@@ -897,7 +897,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(off[q]), "s"(r), "s"(soff) : "memory");
       return;
     }
-    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + ((MODE == 0 || MODE == 15 || MODE == 16) ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + ((MODE == 0 || MODE >= 15) ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
   };
@@ -969,9 +969,23 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
         return n;
       };
       constexpr int VM = n_upto(GA, SA, WG) + n_upto(GB, SB, WG);
-      if constexpr (MODE == 16) {
+      if constexpr (MODE >= 16) {
         // one-MFMA granularity: at most ~1 other instruction after each MFMA
-        // (the issue pattern of the vendor 256x256 kernel); slots s = MFMA index
+        // (the issue pattern of the vendor 256x256 kernel); slots s = MFMA
+        // index.  Per-MODE slot plan: A-k-half-1 reads at 2k (k < 8), barrier 1
+        // after B1, B-k-half-1 reads from B1 + 1 every 2, barrier 2 after B2,
+        // A DMA piece k at DA + SA k, B piece k at DB + SB k, the step-t+1 wait
+        // after W, then the 16 reads of (t+1, k-half 0) spread to slot 126.
+        constexpr int B1 = MODE == 20 ? 19 : 17, B2 = MODE == 20 ? 37 : 35;
+        constexpr int DA = B1 + 2, SA1 = MODE == 17 ? 3 : 4;
+        constexpr int DB = B2 + 2, SB1 = MODE == 17 ? 6 : MODE == 19 ? 7 : 8;
+        constexpr int W = MODE == 18 ? 99 : MODE == 19 ? 97 : 95;
+        auto cnt = [](int d, int st, int w) constexpr {
+          int n = 0;
+          for (int k = 0; k < 8; ++k) n += d + st * k <= w;
+          return n;
+        };
+        constexpr int VMW = cnt(DA, SA1, W) + cnt(DB, SB1, W);
         static_for<128>([&](auto sc) {
           constexpr int S = decltype(sc)::value, IDX = S & 63, I = IDX / 8, J = IDX % 8;
           if constexpr (S < 64) {
@@ -982,22 +996,30 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
           }
           if constexpr (S < 16 && S % 2 == 0)
             read_frag(set1, std::integral_constant<int, S / 2>{}, K1{}, so);
-          if constexpr (S == 17 || S == 35) {
+          if constexpr (S == B1 || S == B2) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
           }
-          if constexpr (S >= 18 && S <= 32 && S % 2 == 0)
-            read_frag(set1, std::integral_constant<int, 8 + (S - 18) / 2>{}, K1{}, so);
-          if constexpr (S >= 19 && S <= 47 && (S - 19) % 4 == 0) dma((S - 19) / 4, ra, soff, slot);
-          if constexpr (S >= 37 && S <= 93 && (S - 37) % 8 == 0) dma(8 + (S - 37) / 8, rb, soff, slot);
-          if constexpr (S == 95) {
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          if constexpr (S > B1 && S <= B1 + 15 && (S - B1 - 1) % 2 == 0)
+            read_frag(set1, std::integral_constant<int, 8 + (S - B1 - 1) / 2>{}, K1{}, so);
+          if constexpr (S >= DA && (S - DA) % SA1 == 0 && (S - DA) / SA1 < 8)
+            dma((S - DA) / SA1, ra, soff, slot);
+          if constexpr (S >= DB && (S - DB) % SB1 == 0 && (S - DB) / SB1 < 8)
+            dma(8 + (S - DB) / SB1, rb, soff, slot);
+          if constexpr (S == W) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
           }
-          if constexpr (S >= 96 && S % 2 == 0)
-            read_frag(set0, std::integral_constant<int, (S - 96) / 2>{}, K0{}, sn);
+          if constexpr (S > W && S < 127) {
+            // read k at slot W + 1 + floor(k (126 - W) / 16)
+            static_for<16>([&](auto kc) {
+              constexpr int Kr = decltype(kc)::value;
+              if constexpr (W + 1 + (Kr * (126 - W)) / 16 == S)
+                read_frag(set0, std::integral_constant<int, Kr>{}, K0{}, sn);
+            });
+          }
           __builtin_amdgcn_sched_barrier(0);
         });
       } else
@@ -1173,6 +1195,10 @@ void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t 
   else if (mode == 14) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 14>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 15) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 15>), dim3(g), dim3(256), 0, s, p);
   else if (mode == 16) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 16>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 20) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 20>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 19) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 19>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 18) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 18>), dim3(g), dim3(256), 0, s, p);
+  else if (mode == 17) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 17>), dim3(g), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
 }
 
