@@ -969,8 +969,9 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
         return n;
       };
       constexpr int VM = n_upto(GA, SA, WG) + n_upto(GB, SB, WG);
-      if constexpr (MODE >= 16) {
-        // one-MFMA granularity: at most ~1 other instruction after each MFMA
+      if constexpr (MODE == 0 || MODE >= 16) {
+        // one-MFMA granularity (production schedule, MODE 0 = 16: +3-6 % over
+        // groups of four MFMAs, profiles/r4k_gemm_ablation.txt): at most ~1 other instruction after each MFMA
         // (the issue pattern of the vendor 256x256 kernel); slots s = MFMA
         // index.  Per-MODE slot plan: A-k-half-1 reads at 2k (k < 8), barrier 1
         // after B1, B-k-half-1 reads from B1 + 1 every 2, barrier 2 after B2,

@@ -36,8 +36,7 @@ def main():
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
-        modes = ((16, "slots"), (17, "slots_dma3_6"), (18, "slots_wait99"), (19, "slots_B7_w97"),
-                 (20, "slots_bar19_37"))
+        modes = ((0, "production"), (1, "no_dma"), (2, "mfma_only"), (14, "burst(r4e)"))
         r = {k: [] for _, k in modes}
         r["hipblaslt"] = []
         for _ in range(5):
