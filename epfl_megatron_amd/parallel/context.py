@@ -109,7 +109,7 @@ def _pair_bwd(q, k, v, o, lse, do, causal, scale):
     o = o.to(q.dtype).contiguous()
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     ext().flash_attn_bwd(do, q, k, v, o, lse.contiguous(), dq, dk, dv, b, sq, sk, nq, nkv, d,
-                         _strides(q, r), _strides(k, 1)[:3], _strides(k, 1)[:3],
+                         _strides(q, r), _strides(k, 1)[:3], _strides(v, 1)[:3],
                          [o.stride(0), o.stride(1), o.stride(2)], bool(causal), float(scale),
                          None, None, None, None)
     return dq.float(), dk.float(), dv.float()
