@@ -649,7 +649,7 @@ bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 // x [M, K] @ w[N, K]^T -> [M, N]
-at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
+at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool packed) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "skinny_gemm: shapes");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "skinny_gemm: contiguous operands");
@@ -660,8 +660,18 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
   TORCH_CHECK(ema::skinny_gemm_supported(M, N, K), "skinny_gemm: unsupported shape");
   check_vec_aligned(x, "x");
   check_vec_aligned(w, "w");
+  TORCH_CHECK(!packed || K % 256 == 0, "skinny_gemm: packed weights need K % 256 == 0");
   auto y = at::empty({M, N}, x.options());
-  ema::skinny_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, dt, cur_stream());
+  ema::SkinnyArgs p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.y = y.data_ptr();
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.ldy = N;
+  p.packed = packed ? 1 : 0;
+  ema::skinny_gemm_ex(p, 0, dt, cur_stream());
   return y;
 }
 
@@ -670,7 +680,8 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w) {
 // 0 plain, 1 residual add (res [M, N]), 2 GLU (-> [M, F]),
 // 3 QKV (-> q [M, nq * hd]; k / v written into the cache slot).
 static ema::SkinnyArgs skinny_args(const at::Tensor& x, const at::Tensor& w,
-                                   const c10::optional<at::Tensor>& norm_w, double eps) {
+                                   const c10::optional<at::Tensor>& norm_w, double eps,
+                                   bool packed) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "skinny: shapes");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "skinny: contiguous operands");
@@ -684,6 +695,8 @@ static ema::SkinnyArgs skinny_args(const at::Tensor& x, const at::Tensor& w,
   p.w = w.data_ptr();
   p.M = (int)x.size(0);
   p.K = (int)x.size(1);
+  TORCH_CHECK(!packed || p.K % 256 == 0, "skinny: packed weights need K % 256 == 0");
+  p.packed = packed ? 1 : 0;
   if (norm_w) {
     TORCH_CHECK(norm_w->is_cuda() && norm_w->is_contiguous() && norm_w->numel() == p.K &&
                 norm_w->scalar_type() == x.scalar_type(), "skinny: norm weight must be [K], x dtype");
@@ -695,8 +708,8 @@ static ema::SkinnyArgs skinny_args(const at::Tensor& x, const at::Tensor& w,
 
 at::Tensor skinny_norm_gemm(const at::Tensor& x, const at::Tensor& w,
                             const c10::optional<at::Tensor>& norm_w, double eps,
-                            const c10::optional<at::Tensor>& res) {
-  auto p = skinny_args(x, w, norm_w, eps);
+                            const c10::optional<at::Tensor>& res, bool packed) {
+  auto p = skinny_args(x, w, norm_w, eps, packed);
   const int64_t N = w.size(0);
   TORCH_CHECK(ema::skinny_gemm_supported(p.M, N, p.K), "skinny: unsupported shape");
   auto y = at::empty({p.M, N}, x.options());
@@ -718,8 +731,9 @@ at::Tensor skinny_norm_gemm(const at::Tensor& x, const at::Tensor& w,
 }
 
 at::Tensor skinny_norm_glu(const at::Tensor& x, const at::Tensor& w1,
-                           const c10::optional<at::Tensor>& norm_w, double eps, int64_t kind) {
-  auto p = skinny_args(x, w1, norm_w, eps);
+                           const c10::optional<at::Tensor>& norm_w, double eps, int64_t kind,
+                           bool packed) {
+  auto p = skinny_args(x, w1, norm_w, eps, packed);
   const int64_t F = w1.size(0) / 2;
   TORCH_CHECK(w1.size(0) == 2 * F && F % 8 == 0 &&
               ema::skinny_gemm_supported(p.M, 2 * F, p.K), "skinny glu: unsupported shape");
@@ -741,8 +755,8 @@ at::Tensor skinny_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w,
                                  int64_t r, int64_t hd, const at::Tensor& cos,
                                  const at::Tensor& sin, const at::Tensor& pos, at::Tensor kcache,
                                  at::Tensor vcache, const c10::optional<at::Tensor>& slot_t,
-                                 int64_t slot) {
-  auto p = skinny_args(x, w, norm_w, eps);
+                                 int64_t slot, bool packed) {
+  auto p = skinny_args(x, w, norm_w, eps, packed);
   const int64_t N = w.size(0);
   TORCH_CHECK(N == ng * (r + 2) * hd && hd % 8 == 0, "skinny qkv: w rows != ng * (r + 2) * hd");
   TORCH_CHECK(ema::skinny_gemm_supported(p.M, N, p.K), "skinny qkv: unsupported shape");
@@ -1128,11 +1142,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("fa_set_stamps", &fa_set_stamps);
   m.def("flash_decode", &flash_decode);
-  m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("packed") = false);
   m.def("skinny_gemm_supported", &skinny_gemm_supported);
-  m.def("skinny_norm_gemm", &skinny_norm_gemm);
-  m.def("skinny_norm_glu", &skinny_norm_glu);
-  m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache);
+  m.def("skinny_norm_gemm", &skinny_norm_gemm, py::arg("x"), py::arg("w"), py::arg("norm_w"),
+        py::arg("eps"), py::arg("res"), py::arg("packed") = false);
+  m.def("skinny_norm_glu", &skinny_norm_glu, py::arg("x"), py::arg("w1"), py::arg("norm_w"),
+        py::arg("eps"), py::arg("kind"), py::arg("packed") = false);
+  m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache, py::arg("x"), py::arg("w"),
+        py::arg("norm_w"), py::arg("eps"), py::arg("ng"), py::arg("r"), py::arg("hd"),
+        py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("kcache"), py::arg("vcache"),
+        py::arg("slot_t"), py::arg("slot"), py::arg("packed") = false);
   m.def("transpose16", &transpose16);
   m.def("transpose16_supported", &transpose16_supported);
 }

@@ -263,6 +263,7 @@ struct SkinnyArgs {
   const int64_t* slot_ptr;  // device slot index (graph decode) or nullptr: `slot`
   int64_t slot;
   int no_halves;        // 1: the persistent GLU keeps full blocks in its last round (A/B)
+  int packed;           // 1: w is in the decode-packed layout (skinny_pack, K % 256 == 0)
 };
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
 

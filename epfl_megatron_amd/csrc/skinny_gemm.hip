@@ -33,6 +33,16 @@
 //     k and v straight into the KV cache slot (device-resident slot index, so
 //     the step is graph-capturable).
 // Shapes: M <= 16, N % 16 == 0, K % 128 == 0 (checked by the host).
+//
+// Packed weights (p.packed, 8-wave forms, K % 256 == 0).  In row-major W a
+// wave's A-operand load (lane L: row L & 15, 8 k at 8 (L >> 4)) touches 16
+// rows x 64 B and every 4-lane quad 4 different cache lines; the streams
+// topped out at 3.9-4.9 TB/s.  skinny_pack (ops/decode_pack.py) stores each
+// (16-row block, wave, k-step) fragment set as one contiguous 1 KiB piece,
+// lane L at byte 16 L, read by the identical MFMA schedule: 4.6-6.0 TB/s on
+// the Llama-2-7B shapes (scripts/gemv_layout_bench.hip,
+// profiles/r4m_gemv_layout.txt).  The k index a lane feeds is unchanged, so X /
+// gamma loads and every epilogue are layout-independent.
 #include <cstdlib>
 #include <type_traits>
 
@@ -129,7 +139,7 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
 #define SKINNY_U 8  // k-steps of W / X (/ gamma) loads in flight per wave
 #endif
 
-template <typename T, int WAVES, bool NORM, int EPI, int ACT>
+template <typename T, int WAVES, bool NORM, int EPI, int ACT, bool PACKED>
 __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
   constexpr int U = SKINNY_U;
@@ -141,11 +151,16 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
   const T* __restrict__ w = (const T*)p.w;
   const int kq = K / WAVES, kbeg = wave * kq;
   const int r = lane & 15, kc = 8 * (lane >> 4);  // fragment row / k offset of this lane
-  const T* wr = w + w_row<EPI>(blockIdx.x, r, N) * K + kbeg + kc;
+  const int steps = kq / 32;
+  // W fragment of k-step s at wr + WS s: row-major rows, or the packed
+  // layout's contiguous 1 KiB per (block, wave, step) (skinny_pack)
+  constexpr int WS = PACKED ? 512 : 32;
+  static_assert(!PACKED || WAVES == 8, "the packed layout is cut for 8 waves");
+  const T* wr = PACKED ? w + ((int64_t)blockIdx.x * WAVES + wave) * steps * 512 + 8 * lane
+                       : w + w_row<EPI>(blockIdx.x, r, N) * K + kbeg + kc;
   const bool xon = r < M;
   const T* xr = x + (int64_t)(xon ? r : 0) * K + kbeg + kc;
   const T* gr = NORM ? (const T*)p.norm_w + kbeg + kc : nullptr;
-  const int steps = kq / 32;
   const int nblk = steps / U;  // full ring blocks; the < U leftover steps run after them
 
   // Ring of U k-steps: the W fragment (nontemporal: each weight byte is read
@@ -158,7 +173,7 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
   if (nblk > 0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
+      a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * u));
       xv[u] = *reinterpret_cast<const x8*>(xr + 32 * u);
       if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * u);
     }
@@ -220,7 +235,7 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
       acc = mfma16x16x32<T>(a[u], bop(xv[u], gv[u]), acc);
       if constexpr (REFILL) {
         const int s = (blk + 1) * U + u;
-        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * s));
+        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * s));
         xv[u] = *reinterpret_cast<const x8*>(xr + 32 * s);
         if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * s);
       }
@@ -238,7 +253,7 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
 #pragma unroll
     for (int u = 0; u < U - 1; ++u) {
       if (u < left) {
-        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * (s0 + u)));
+        a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * (s0 + u)));
         xv[u] = *reinterpret_cast<const x8*>(xr + 32 * (s0 + u));
         if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + u));
       }
@@ -269,7 +284,7 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
 //     the next block's first U k-steps, so the stream never drains;
 //   * per block, the 8 partial tiles meet in a double-buffered LDS slot and
 //     wave 0 runs the epilogue while the other waves stream the next block.
-template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U>
+template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U, bool PACKED>
 __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
   constexpr int WAVES = 8;
@@ -292,13 +307,17 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   // at most 5.5 instead of 6 block times per workgroup).  A half block's MFMA
   // rows r and r + 4 read the same W row (one HBM fetch per cache line).
   const int nrem = nblocks % G;
-  const bool halves = EPI == EPI_GLU && nrem > 0 && 2 * nrem <= G && !p.no_halves;
+  // (not with PACKED: a half block's 8 W rows are spread over the whole packed
+  // 1 KiB pieces of its 16-row block, so it would stream the full block)
+  const bool halves = EPI == EPI_GLU && !PACKED && nrem > 0 && 2 * nrem <= G && !p.no_halves;
   const int rounds = halves ? (nblocks - nrem) / G : 0;
   const int nunits = halves ? rounds + (wg < 2 * nrem ? 1 : 0) : (nblocks - wg + G - 1) / G;
   auto unit_blk = [&](int j) { return j < rounds || !halves ? wg + j * G : nblocks - nrem + wg / 2; };
   auto unit_half = [&](int j) { return j < rounds || !halves ? -1 : (wg & 1); };
+  constexpr int WS = PACKED ? 512 : 32;  // elements between a lane's k-steps
   auto wptr = [&](int j) {
     const int b = unit_blk(j), h = unit_half(j);
+    if constexpr (PACKED) return w + ((int64_t)b * WAVES + wave) * STEPS * 512 + 8 * lane;
     int64_t row;
     if (h < 0) row = w_row<EPI>(b, r, N);
     else row = (r < 8 ? 0 : (int64_t)N) + (int64_t)b * 8 + 4 * h + (r & 3);
@@ -310,7 +329,7 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
 
   x8 a[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + 32 * u));
+  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * u));
   x8 xs[STEPS];
   {
     const T* xr = x + (int64_t)r * K + kbeg + kc;
@@ -370,7 +389,7 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
     for (int s = 0; s < STEPS; ++s) {
       acc = mfma16x16x32<T>(a[s % U], xs[s], acc);
       if (!LAST || s + U < STEPS) {
-        const T* src = s + U < STEPS ? wr + 32 * (s + U) : wn + 32 * (s + U - STEPS);
+        const T* src = s + U < STEPS ? wr + WS * (s + U) : wn + WS * (s + U - STEPS);
         a[s % U] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(src));
       }
       __builtin_amdgcn_sched_barrier(0);  // {MFMA s, refill s} in program order
@@ -413,22 +432,25 @@ template <typename T, int WAVES, int STEPS, bool NORM, int EPI, int ACT>
 void launch(const SkinnyArgs& p, hipStream_t s) {
   const int nblocks = EPI == EPI_GLU ? p.N / 8 : p.N / 16;
   if constexpr (STEPS == 0) {
-    hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT>), dim3((unsigned)nblocks),
+    if constexpr (WAVES == 8) {
+      if (p.packed) {
+        hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, true>), dim3((unsigned)nblocks),
+                           dim3(64 * WAVES), 0, s, p);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, false>), dim3((unsigned)nblocks),
                        dim3(64 * WAVES), 0, s, p);
   } else {
     // ring depth (k-steps of weight loads in flight per wave): 16 (batch-1 graph decode
-    // 301 -> 308 tok/s over 8, profiles/r3s_skinny_ring_depth.txt); EMA_SKINNY_PU=8 for A/B
-    static const int pu = [] {
-      const char* e = getenv("EMA_SKINNY_PU");
-      return e ? atoi(e) : 16;
-    }();
+    // 301 -> 308 tok/s over 8, profiles/r3s_skinny_ring_depth.txt)
     const int g = nblocks < num_cus() ? nblocks : num_cus();
-    if (pu == 16)
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16>), dim3((unsigned)g), dim3(512),
-                         0, s, p);
+    if (p.packed)
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16, true>), dim3((unsigned)g),
+                         dim3(512), 0, s, p);
     else
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 8>), dim3((unsigned)g), dim3(512),
-                         0, s, p);
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16, false>), dim3((unsigned)g),
+                         dim3(512), 0, s, p);
   }
 }
 
@@ -491,7 +513,8 @@ void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
     const char* e = getenv("EMA_SKINNY_PERSIST");
     return !(e && e[0] == '0');
   }();
-  const bool w8 = want == 8 && p.K % 256 == 0;
+  // packed weights are cut for the 8-wave forms (the host checks K % 256 == 0)
+  const bool w8 = (want == 8 || p.packed) && p.K % 256 == 0;
   const int steps = w8 ? p.K / 256 : 0;
   if (persist && w8 && (steps == 16 || steps == 32)) {
     if (dt == DT_BF16) steps == 16 ? dispatch<bf16, 8, 16>(p, epi, s) : dispatch<bf16, 8, 32>(p, epi, s);

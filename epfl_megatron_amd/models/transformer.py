@@ -37,6 +37,7 @@ from ..ops._ext import use_native, ext
 from ..parallel.context import chunk_position_ids, ring_attention
 from ..ops.attention import flash_attn_qkvpacked, flash_attn_func, flash_decode_cached
 from ..ops.activations import glu, bias_gelu, gelu
+from ..ops import decode_pack
 from ..ops.softmax import FusedScaleMaskSoftmax
 from .enums import AttnMaskType, AttnType, LayerType, ModelType, PositionEmbeddingType
 from .module import MegatronModule
@@ -511,9 +512,15 @@ class ParallelTransformerLayer(MegatronModule):
             pos = position_ids[:, -1:].long()
         graph = getattr(ip, "device_offset", None) is not None
         ng, r, hd = sa.num_groups_per_partition, sa.q_per_group, sa.hidden_size_per_attention_head
-        q = C.skinny_qkv_rope_cache(x, sa.query_key_value.weight, ln1.weight, ln1.eps, ng, r, hd,
+        # weights in the decode-packed layout when the shape allows (ops/decode_pack.py)
+        wq, wo = sa.query_key_value.weight, sa.dense.weight
+        w1, w2 = mlp.dense_h_to_4h.weight, mlp.dense_4h_to_h.weight
+        pq, po = decode_pack.packed(wq), decode_pack.packed(wo)
+        p1, p2 = decode_pack.packed(w1, glu=True), decode_pack.packed(w2)
+        q = C.skinny_qkv_rope_cache(x, wq if pq is None else pq, ln1.weight, ln1.eps, ng, r, hd,
                                     cos, sin, pos, kc, vc,
-                                    ip.device_offset if graph else None, 0 if graph else s0)
+                                    ip.device_offset if graph else None, 0 if graph else s0,
+                                    pq is not None)
         q4 = q.view(b, 1, ng * r, hd)
         if graph:
             o = flash_decode_cached(q4, kc.transpose(0, 1), vc.transpose(0, 1), ip.device_kv_len)
@@ -528,11 +535,13 @@ class ParallelTransformerLayer(MegatronModule):
         # (one persistent launch with grid barriers for these three products was
         # measured 2.6x slower than the three launches: profiles/r3x_decode_mlp_fused.txt)
         first = state.get_tensor_model_parallel_rank() == 0
-        h2 = C.skinny_norm_gemm(o.reshape(b, -1), sa.dense.weight, None, 0.0, x if first else None)
+        h2 = C.skinny_norm_gemm(o.reshape(b, -1), wo if po is None else po, None, 0.0,
+                                x if first else None, po is not None)
         h2 = tp.reduce_from_tensor_model_parallel_region(h2)
-        y = C.skinny_norm_glu(h2, mlp.dense_h_to_4h.weight, ln2.weight, ln2.eps,
-                              tp.layers._GLU_KIND[mlp.glu_activation])
-        h3 = C.skinny_norm_gemm(y, mlp.dense_4h_to_h.weight, None, 0.0, h2 if first else None)
+        y = C.skinny_norm_glu(h2, w1 if p1 is None else p1, ln2.weight, ln2.eps,
+                              tp.layers._GLU_KIND[mlp.glu_activation], p1 is not None)
+        h3 = C.skinny_norm_gemm(y, w2 if p2 is None else p2, None, 0.0, h2 if first else None,
+                                p2 is not None)
         h3 = tp.reduce_from_tensor_model_parallel_region(h3)
         return h3.view(1, b, H)
 

@@ -1,0 +1,79 @@
+"""Decode-packed weight layout for the weight-streaming skinny GEMM.
+
+A decode step multiplies <= 16 rows by every weight of the model, so its time
+is the weight stream from HBM (reference: ``megatron/text_generation/
+generation.py:179-264`` runs the same step through the training GEMMs).  The
+skinny kernel (``csrc/skinny_gemm.hip``) feeds ``v_mfma_f32_16x16x32`` with
+lane L holding 8 consecutive k of W row ``L & 15``: on a row-major ``[N, K]``
+weight one wave-load touches 16 rows x 64 B (every 4-lane quad four cache
+lines) and the stream tops out at 3.9-4.9 TB/s.  ``pack`` reorders W so that
+the fragments one wave loads for one k-step are a contiguous 1 KiB piece
+(lane L at byte 16 L); the kernel's MFMA schedule and the k index each lane
+feeds are unchanged, and the stream reaches 4.6-6.0 TB/s
+(``scripts/gemv_layout_bench.hip``, ``profiles/r4m_gemv_layout.txt``).
+
+Layout (K % 256 == 0, S = K / 256 k-steps of 32 per wave, 8 waves):
+``packed[b, wave, s, q, r, e] = W[row(b, r), wave * 32 S + 32 s + 8 q + e]``
+with ``row(b, r) = 16 b + r`` (plain / QKV) or, for a GLU weight ``[2F, K]``,
+``8 b + r`` (up) / ``F + 8 b + r - 8`` (gate) — the kernel's ``w_row``.
+
+The packed copy lives next to the parameter (``_ema_decode_packed``) and is
+rebuilt when the parameter's storage or in-place version changes, i.e. after
+an optimizer step or a checkpoint load; 288 GB of HBM holds both layouts of a
+70B TP8 shard many times over.  ``EMA_SKINNY_PACK=0`` streams the row-major
+weights instead (A/B).
+"""
+import os
+
+import torch
+
+ENABLED = os.environ.get("EMA_SKINNY_PACK", "1") != "0"
+
+
+def packable(w):
+    """W [N, K] the packed 8-wave skinny forms can read."""
+    return (w.dim() == 2 and w.shape[1] % 256 == 0 and w.shape[0] % 16 == 0
+            and w.dtype in (torch.bfloat16, torch.float16))
+
+
+def pack(w, glu=False):
+    """The packed copy of ``w`` ([N, K] -> [N, K], same dtype / device)."""
+    assert packable(w), f"skinny pack: unsupported weight {tuple(w.shape)} {w.dtype}"
+    n, k = w.shape
+    s = k // 256
+    if glu:
+        f = n // 2
+        blocks = torch.stack((w[:f].reshape(f // 8, 8, k), w[f:].reshape(f // 8, 8, k)), 1)
+        blocks = blocks.reshape(f // 8, 16, k)
+    else:
+        blocks = w.reshape(n // 16, 16, k)
+    nb = blocks.shape[0]
+    # [b, r, wave, s, q, e] -> [b, wave, s, q, r, e]: lane q * 16 + r
+    return blocks.reshape(nb, 16, 8, s, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous().reshape(n, k)
+
+
+def unpack(p, glu=False):
+    """Inverse of ``pack`` (tests)."""
+    n, k = p.shape
+    s = k // 256
+    nb = n // 16
+    blocks = p.reshape(nb, 8, s, 4, 16, 8).permute(0, 4, 1, 2, 3, 5).reshape(nb, 16, k)
+    if glu:
+        f = n // 2
+        return torch.cat((blocks[:, :8].reshape(f, k), blocks[:, 8:].reshape(f, k)), 0)
+    return blocks.reshape(n, k)
+
+
+def packed(w, glu=False):
+    """Cached packed copy of parameter ``w``, or None when the row-major
+    weight must be streamed (disabled / unsupported shape)."""
+    if not ENABLED or not packable(w):
+        return None
+    key = (w.data_ptr(), w._version, bool(glu), w.dtype, tuple(w.shape))
+    hit = getattr(w, "_ema_decode_packed", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        p = pack(w.detach(), glu)
+    w._ema_decode_packed = (key, p)
+    return p

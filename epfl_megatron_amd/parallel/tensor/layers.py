@@ -44,6 +44,7 @@ from .mappings import (copy_to_tensor_model_parallel_region,
 from .random import get_cuda_rng_tracker
 from .utils import VocabUtility
 from ...ops._ext import ext
+from ...ops import decode_pack
 
 _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {
     "tensor_model_parallel": False,
@@ -756,7 +757,9 @@ def _skinny_linear(input_, weight, bias, sequence_parallel):
     x2 = input_.reshape(m, k)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
-    out = ext().skinny_gemm(x2, weight).view(*input_.shape[:-1], weight.shape[0])
+    wp = decode_pack.packed(weight)  # decode-packed copy (ops/decode_pack.py) or None
+    out = ext().skinny_gemm(x2, weight if wp is None else wp, wp is not None)
+    out = out.view(*input_.shape[:-1], weight.shape[0])
     return out if bias is None else out + bias
 
 

@@ -569,6 +569,50 @@ def test_skinny_fused_qkv_rope_cache(ng, r, hd, graph_slot):
     assert torch.equal(kmem[keep], k0[keep]) and torch.equal(vmem[keep], v0[keep])
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 12288, 4096), (16, 4096, 11008),
+                                   (3, 1024, 8192), (5, 512, 512)])
+def test_skinny_packed_weights_match_row_major(M, N, K):
+    """The decode-packed weight layout (ops/decode_pack.py) feeds every lane
+    the same k indices in the same order as the row-major stream: plain,
+    norm + residual, norm + GLU and QKV + RoPE + cache outputs are bit-equal
+    across the persistent (K = 4096 / 8192) and per-block (K = 11008 / 512)
+    forms."""
+    from epfl_megatron_amd.ops import decode_pack
+    from epfl_megatron_amd.ops.rope import rope_table
+    C = _ext()
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    g = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    wp = decode_pack.pack(w)
+    assert torch.equal(decode_pack.unpack(wp), w)
+    with torch.no_grad():
+        assert torch.equal(C.skinny_gemm(x, wp, True), C.skinny_gemm(x, w))
+        assert torch.equal(C.skinny_norm_gemm(x, wp, g, 1e-5, res, True),
+                           C.skinny_norm_gemm(x, w, g, 1e-5, res))
+        for kind in (0, 1):
+            assert torch.equal(C.skinny_norm_glu(x, decode_pack.pack(w, glu=True), g, 1e-6, kind, True),
+                               C.skinny_norm_glu(x, w, g, 1e-6, kind)), kind
+        hd = 128
+        if N % (3 * hd) == 0:
+            ng = N // (3 * hd)
+            cos, sin = rope_table(hd, 64, DEV)
+            pos = torch.arange(M, device=DEV).view(M, 1) + 3
+            caches = [torch.zeros(8, M, ng, hd, device=DEV, dtype=torch.bfloat16) for _ in range(4)]
+            qa = C.skinny_qkv_rope_cache(x, wp, g, 1e-5, ng, 1, hd, cos, sin, pos, caches[0],
+                                         caches[1], None, 2, True)
+            qb = C.skinny_qkv_rope_cache(x, w, g, 1e-5, ng, 1, hd, cos, sin, pos, caches[2],
+                                         caches[3], None, 2)
+            assert torch.equal(qa, qb) and torch.equal(caches[0], caches[2])
+            assert torch.equal(caches[1], caches[3])
+    # the cached copy follows in-place updates of the parameter
+    p1 = decode_pack.packed(w)
+    assert p1 is decode_pack.packed(w)
+    w.mul_(2)
+    assert torch.equal(decode_pack.packed(w), decode_pack.pack(w))
+
+
 def test_flash_attention_kvcache_causal_offset():
     """sq < sk (decode with cache): bottom-right aligned causal mask."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref

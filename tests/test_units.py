@@ -435,3 +435,22 @@ def test_rccl_watchdog_env():
     assert env["TORCH_NCCL_ENABLE_MONITORING"] == "1"
     assert env["TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC"] == "600"
     assert env["TORCH_NCCL_DUMP_ON_TIMEOUT"] == "1"
+
+
+def test_decode_pack_layout():
+    """ops/decode_pack.py: 1 KiB per (16-row block, wave, k-step), lane
+    q * 16 + r holding W[row(b, r), 32 S wave + 32 s + 8 q : +8]; GLU blocks
+    interleave 8 up and 8 gate rows; unpack inverts pack."""
+    from epfl_megatron_amd.ops import decode_pack as dp
+    torch.manual_seed(0)
+    S = 2
+    for glu in (False, True):
+        w = torch.randn(64, 256 * S).bfloat16()
+        p = dp.pack(w, glu)
+        assert p.shape == w.shape and torch.equal(dp.unpack(p, glu), w)
+        pv = p.view(-1, 8, S, 4, 16, 8)
+        for (b, wv, s, q, r, e) in [(0, 0, 0, 0, 0, 0), (1, 3, 1, 2, 9, 5), (3, 7, 1, 3, 15, 7)]:
+            row = (8 * b + r if r < 8 else 32 + 8 * b + r - 8) if glu else 16 * b + r
+            assert pv[b, wv, s, q, r, e] == w[row, wv * 32 * S + 32 * s + 8 * q + e]
+    assert not dp.packable(torch.zeros(16, 384).bfloat16())
+    assert not dp.packable(torch.zeros(16, 512))
