@@ -567,8 +567,6 @@ def _derive_recompute_and_parallel_features(args):
         _require(args.seq_length % (2 * cp) == 0,
                  f"seq_length ({args.seq_length}) is not divisible by 2 x context parallel "
                  f"size ({cp}) (zig-zag sequence split)")
-        _require(not args.reset_attention_mask,
-                 "--reset_attention_mask is not supported with context parallelism")
         _require(not sim_tp, "--simulated_tensor_parallel_size excludes context parallelism")
         # the ring-attention pair kernels apply no attention dropout:
         # refuse a configuration whose CP=1 counterpart would drop attention probs

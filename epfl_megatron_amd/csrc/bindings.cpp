@@ -510,6 +510,7 @@ ema::AttnParams make_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   p.v_sb = vs[0]; p.v_ss = vs[1]; p.v_sg = vs[2];
   p.o_sb = os[0]; p.o_ss = os[1]; p.o_sh = os[2];
   p.causal = causal ? 1 : 0;
+  p.coff = (int)(sk - sq);
   p.scale = (float)scale;
   p.lse_sb = nq * sq;
   p.lse_sh = sq;
@@ -580,7 +581,8 @@ void flash_attn_fwd_merge(const at::Tensor& q, const at::Tensor& k, const at::Te
                           at::Tensor o32, at::Tensor lse, int64_t b, int64_t sq, int64_t sk,
                           int64_t nq, int64_t nkv, int64_t hd, std::vector<int64_t> qs,
                           std::vector<int64_t> ks, std::vector<int64_t> vs, bool causal,
-                          double scale, bool merge) {
+                          double scale, bool merge, const c10::optional<at::Tensor>& docs,
+                          int64_t coff) {
   check_gpu(q, "q");
   TORCH_CHECK(o32.scalar_type() == at::kFloat && o32.dim() == 4 && o32.size(0) == b &&
                   o32.size(1) == sq && o32.size(2) == nq && o32.size(3) == hd && o32.stride(3) == 1 &&
@@ -607,6 +609,11 @@ void flash_attn_fwd_merge(const at::Tensor& q, const at::Tensor& k, const at::Te
   p.o32_ss = o32.stride(1);
   p.o32_sh = o32.stride(2);
   p.merge = merge ? 1 : 0;
+  set_docs(p, docs);
+  if (coff >= 0) {
+    TORCH_CHECK(causal && coff >= sk - sq, "flash_attn_fwd_merge: coff needs the causal kernel");
+    p.coff = (int)coff;
+  }
   ema::flash_attn_fwd(p, dtype_code(q), cur_stream());
 }
 
@@ -618,11 +625,15 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
                     const c10::optional<at::Tensor>& rope_cos,
                     const c10::optional<at::Tensor>& rope_sin,
                     const c10::optional<at::Tensor>& rope_pos,
-                    const c10::optional<at::Tensor>& docs) {
+                    const c10::optional<at::Tensor>& docs, int64_t coff) {
   check_gpu(q, "q");
   auto f = make_attn(q, k, v, out, lse, b, sq, sk, nq, nkv, hd, qs, ks, vs, os, causal, scale);
   set_rope(f, rope_cos, rope_sin, rope_pos);
   set_docs(f, docs);
+  if (coff >= 0) {
+    TORCH_CHECK(causal && coff >= sk - sq, "flash_attn_bwd: coff needs the causal kernel");
+    f.coff = (int)coff;
+  }
   TORCH_CHECK(dout.scalar_type() == q.scalar_type(), "dout dtype mismatch");
   TORCH_CHECK(dout.stride(-1) == 1, "dout head_dim must be contiguous");
   ema::AttnBwdParams p{};
@@ -732,11 +743,13 @@ at::Tensor skinny_norm_gemm(const at::Tensor& x, const at::Tensor& w,
 
 at::Tensor skinny_norm_glu(const at::Tensor& x, const at::Tensor& w1,
                            const c10::optional<at::Tensor>& norm_w, double eps, int64_t kind,
-                           bool packed) {
+                           bool packed, int64_t packed_tail) {
   auto p = skinny_args(x, w1, norm_w, eps, packed);
   const int64_t F = w1.size(0) / 2;
   TORCH_CHECK(w1.size(0) == 2 * F && F % 8 == 0 &&
               ema::skinny_gemm_supported(p.M, 2 * F, p.K), "skinny glu: unsupported shape");
+  TORCH_CHECK(!packed || packed_tail == ema::skinny_glu_half_tail(F, p.K, norm_w.has_value()),
+              "skinny glu: weight packed for another half-unit tail (skinny_glu_half_tail)");
   auto y = at::empty({p.M, F}, x.options());
   p.N = (int)F;
   p.y = y.data_ptr();
@@ -803,7 +816,8 @@ at::Tensor skinny_qkv_rope_cache(const at::Tensor& x, const at::Tensor& w,
 void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor out,
                   int64_t b, int64_t sk, int64_t nq, int64_t nkv, int64_t hd,
                   std::vector<int64_t> qs, std::vector<int64_t> ks, std::vector<int64_t> vs,
-                  std::vector<int64_t> os, double scale, const c10::optional<at::Tensor>& kv_len) {
+                  std::vector<int64_t> os, double scale, const c10::optional<at::Tensor>& kv_len,
+                  int64_t kpw) {
   check_gpu(q, "q");
   if (kv_len) {
     TORCH_CHECK(kv_len->is_cuda() && kv_len->scalar_type() == at::kInt && kv_len->numel() >= 1,
@@ -818,6 +832,8 @@ void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   TORCH_CHECK(q.stride(-1) == 1 && k.stride(-1) == 1 && v.stride(-1) == 1 && out.stride(-1) == 1,
               "head_dim must be contiguous");
   for (int64_t s : ks) TORCH_CHECK(s % 8 == 0, "k strides must keep 16-byte alignment");
+  TORCH_CHECK(qs[0] % 8 == 0 && qs[2] % 8 == 0 && qs[3] % 8 == 0,
+              "q strides must keep 16-byte alignment");
   for (const at::Tensor* t : {&q, &k, &v}) check_vec_aligned(*t, "q/k/v");
   auto span = [](int64_t b, int64_t s, int64_t n, int64_t sb, int64_t ss, int64_t sn, int64_t hd) {
     return (b - 1) * sb + (s - 1) * ss + (n - 1) * sn + hd;
@@ -835,10 +851,24 @@ void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   p.o_sb = os[0]; p.o_sh = os[2];
   p.scale = (float)scale;
   p.kv_len = kv_len ? kv_len->data_ptr<int>() : nullptr;
-  const int64_t ns = ema::flash_decode_splits((int)sk);
+  // keys per wave: auto (the largest of 64 / 16 / 8 whose grid covers the chip) or forced (A/B)
+  if (kpw <= 0) kpw = ema::flash_decode_kpw((int)b, (int)sk, (int)nq, (int)nkv);
+  TORCH_CHECK(kpw == 8 || kpw == 16 || kpw == 64, "decode attention: kpw must be 8, 16 or 64");
+  p.kpw = (int)kpw;
+  const int64_t ns = ema::flash_decode_splits((int)sk, (int)kpw);
   auto ws = at::empty({b * nq * ns * (hd + 2)}, q.options().dtype(at::kFloat));
   p.ws_o = ws.data_ptr<float>();
   p.ws_ml = p.ws_o + b * nq * ns * hd;
+  // arrival counters: zeroed once, re-armed by the kernel; one buffer per
+  // device that only grows (a hipGraph-captured step keeps its pointer: the
+  // eager warm-up before capture sizes it)
+  static std::vector<at::Tensor> counters;
+  const int dev = q.get_device();
+  if ((int)counters.size() <= dev) counters.resize(dev + 1);
+  const int64_t nc = ema::flash_decode_counters((int)b, (int)nq, (int)nkv);
+  if (!counters[dev].defined() || counters[dev].numel() < nc)
+    counters[dev] = at::zeros({std::max<int64_t>(nc, 4096)}, q.options().dtype(at::kInt));
+  p.counters = reinterpret_cast<unsigned*>(counters[dev].data_ptr<int>());
   ema::flash_decode(p, dtype_code(q), cur_stream());
 }
 
@@ -1138,16 +1168,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_fwd", &bias_dropout_add_fwd);
   m.def("bias_dropout_add_bwd", &bias_dropout_add_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_fwd_merge", &flash_attn_fwd_merge);
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_fwd_merge", &flash_attn_fwd_merge, py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("o32"), py::arg("lse"), py::arg("b"), py::arg("sq"), py::arg("sk"), py::arg("nq"),
+        py::arg("nkv"), py::arg("hd"), py::arg("qs"), py::arg("ks"), py::arg("vs"),
+        py::arg("causal"), py::arg("scale"), py::arg("merge"), py::arg("docs") = py::none(),
+        py::arg("coff") = -1);
+  m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"),
+        py::arg("v"), py::arg("out"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
+        py::arg("b"), py::arg("sq"), py::arg("sk"), py::arg("nq"), py::arg("nkv"), py::arg("hd"),
+        py::arg("qs"), py::arg("ks"), py::arg("vs"), py::arg("os"), py::arg("causal"),
+        py::arg("scale"), py::arg("rope_cos"), py::arg("rope_sin"), py::arg("rope_pos"),
+        py::arg("docs"), py::arg("coff") = -1);
   m.def("fa_set_stamps", &fa_set_stamps);
-  m.def("flash_decode", &flash_decode);
+  m.def("flash_decode", &flash_decode, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"),
+        py::arg("b"), py::arg("sk"), py::arg("nq"), py::arg("nkv"), py::arg("hd"), py::arg("qs"),
+        py::arg("ks"), py::arg("vs"), py::arg("os"), py::arg("scale"), py::arg("kv_len"),
+        py::arg("kpw") = 0);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("packed") = false);
   m.def("skinny_gemm_supported", &skinny_gemm_supported);
   m.def("skinny_norm_gemm", &skinny_norm_gemm, py::arg("x"), py::arg("w"), py::arg("norm_w"),
         py::arg("eps"), py::arg("res"), py::arg("packed") = false);
   m.def("skinny_norm_glu", &skinny_norm_glu, py::arg("x"), py::arg("w1"), py::arg("norm_w"),
-        py::arg("eps"), py::arg("kind"), py::arg("packed") = false);
+        py::arg("eps"), py::arg("kind"), py::arg("packed") = false, py::arg("packed_tail") = 0);
+  m.def("skinny_glu_half_tail", &ema::skinny_glu_half_tail);
   m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache, py::arg("x"), py::arg("w"),
         py::arg("norm_w"), py::arg("eps"), py::arg("ng"), py::arg("r"), py::arg("hd"),
         py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("kcache"), py::arg("vcache"),

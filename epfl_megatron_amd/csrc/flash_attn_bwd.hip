@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv2_k(const AttnBwdParams P) 
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, l4 = (lane >> 4) & 1;
   const int S = P.kv_split > 1 ? P.kv_split : 1;
   const int r = p.nq / p.nkv, r_per = r / S;
-  const int off = p.sk - p.sq;
+  const int off = p.coff;
   const float sl2 = p.scale * 1.4426950408889634f;
   const int ngs = p.nkv * S;
   const int nitems = ((p.sk + BNK - 1) / BNK) * ngs * p.b;
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   const int qb = CAUSAL ? (nqb - 1 - lin / nhb) : lin / nhb;
   const int head = (lin % nhb) % p.nq, b = (lin % nhb) / p.nq;
   const int r = p.nq / p.nkv, g = head / r, hh = head - g * r;
-  const int off = p.sk - p.sq;
+  const int off = p.coff;
   const int q0w = qb * BMW + wave * 32;
   const int qrow = q0w + c;
   const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   const int hb = lin % nhb;
   const int head = hb % p.nq, b = hb / p.nq;
   const int r = p.nq / p.nkv, g = head / r;
-  const int off = p.sk - p.sq;
+  const int off = p.coff;
 
   const T* Q = (const T*)p.q + (int64_t)b * p.q_sb + (int64_t)g * p.q_sg + (int64_t)(head % r) * p.q_sh;
   const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
@@ -194,7 +194,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
           });
         });
       });
-      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax) : (n0 + KT > p.sk);
+      // (causal: the key-count bound only binds when the diagonal offset
+      // reaches past sk, i.e. a context-parallel pair run with coff = sk)
+      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax || n0 + KT > p.sk)
+                                    : (n0 + KT > p.sk);
       if (need_mask) {
         // element i of s0 is key n0 + acc_row(i, h), of s1 that + 32: with
         // rc = acc_row(i, 0) the tests are rc <= hi and rc >= lo, one compare

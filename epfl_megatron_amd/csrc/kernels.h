@@ -138,6 +138,10 @@ struct AttnParams {
   float* o32;
   int64_t o32_sb, o32_ss, o32_sh;
   int merge;
+  // causal diagonal offset: key k is visible to query q iff k <= q + coff
+  // (default sk - sq, bottom-right aligned; a context-parallel pair whose keys
+  // all precede its queries passes sk: no causal cut, document starts only)
+  int coff;
 };
 struct AttnBwdParams {
   AttnParams f;
@@ -187,8 +191,15 @@ struct DecodeParams {
   // sized for sk (the cache capacity) and chunks past the length exit early,
   // so one launch serves every step of a captured hipGraph decode loop.
   const int* kv_len;
+  // zeroed uint32 [flash_decode_counters()]: arrivals per (batch, head slice)
+  // when a sequence is split over several workgroups; the last one to arrive
+  // combines the chunk partials and re-arms its counter
+  unsigned* counters;
+  int kpw;  // keys per wave: 64 / 16 / 8 (flash_decode_kpw picks; chunk = 4 kpw keys)
 };
-int flash_decode_splits(int sk);
+int flash_decode_kpw(int b, int sk, int nq, int nkv);
+int flash_decode_splits(int sk, int kpw);
+int flash_decode_counters(int b, int nq, int nkv);
 void flash_decode(const DecodeParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
@@ -262,10 +273,10 @@ struct SkinnyArgs {
   int64_t c_ss, c_sb;
   const int64_t* slot_ptr;  // device slot index (graph decode) or nullptr: `slot`
   int64_t slot;
-  int no_halves;        // 1: the persistent GLU keeps full blocks in its last round (A/B)
   int packed;           // 1: w is in the decode-packed layout (skinny_pack, K % 256 == 0)
 };
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
+int skinny_glu_half_tail(int64_t F, int64_t K, bool norm);
 
 // ---- transpose.hip -------------------------------------------------------------------------------
 // dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.

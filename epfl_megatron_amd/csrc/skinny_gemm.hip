@@ -73,9 +73,50 @@ __device__ __forceinline__ int64_t w_row(int blk, int r, int N) {
 
 // Output of one 16-feature block (t = the block's reduced fp32 tile; lane
 // holds column m = lane & 15, features 4 (lane >> 4) + i).
+// The epilogue's global operands for one block, loaded ahead (before the
+// block's k-loop) by the wave that runs the epilogue, so the epilogue does not
+// wait out load round trips while the other waves stream the next block: the
+// residual tile (EPI_RES) or the rotary cos / sin pairs (EPI_QKV; the token
+// positions and the cache slot once per workgroup).
+template <typename T, int EPI>
+struct EpiPre {
+  typename fa::MT<T>::x4 rv{};
+  float c[2] = {0.f, 0.f}, s[2] = {0.f, 0.f};
+  int64_t pos = 0, slot = 0;
+};
+
+template <typename T, int EPI>
+__device__ __forceinline__ void epi_init(const SkinnyArgs& p, int lane, EpiPre<T, EPI>& e) {
+  if constexpr (EPI == EPI_QKV) {
+    const int m = lane & 15;
+    e.pos = m < p.M ? p.pos[(int64_t)m * p.pos_sb] : 0;
+    e.slot = p.slot_ptr ? *p.slot_ptr : p.slot;
+  }
+}
+
+template <typename T, int EPI>
+__device__ __forceinline__ void epi_prefetch(const SkinnyArgs& p, int blk, int lane, EpiPre<T, EPI>& e) {
+  const int m = lane & 15, n = blk * 16 + 4 * (lane >> 4);
+  if (m >= p.M) return;
+  if constexpr (EPI == EPI_RES) {
+    e.rv = *reinterpret_cast<const typename fa::MT<T>::x4*>((const T*)p.res + (int64_t)m * p.ldr + n);
+  }
+  if constexpr (EPI == EPI_QKV) {
+    const int hd = p.hd, per_g = (p.r + 2) * hd;
+    const int d = (n - (n / per_g) * per_g) % hd;
+    const float* cr = p.cos + e.pos * (hd / 2) + d / 2;
+    const float* sr = p.sin + e.pos * (hd / 2) + d / 2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      e.c[j] = cr[j];
+      e.s[j] = sr[j];
+    }
+  }
+}
+
 template <typename T, int EPI, int ACT>
 __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4& t, int lane,
-                                         int half = -1) {
+                                         int half = -1, const EpiPre<T, EPI>* pre = nullptr) {
   const int M = p.M;
   // D layout: lane holds column m = lane & 15, rows (features) 4 (lane >> 4) + i
   const int m = lane & 15, nr = 4 * (lane >> 4);
@@ -102,7 +143,7 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
   if (m >= M) return;
   const int n = blk * 16 + nr;
   if constexpr (EPI == EPI_RES) {
-    const typename fa::MT<T>::x4 rv =
+    const typename fa::MT<T>::x4 rv = pre ? pre->rv :
         *reinterpret_cast<const typename fa::MT<T>::x4*>((const T*)p.res + (int64_t)m * p.ldr + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = (T)((float)o[i] + (float)rv[i]);
@@ -111,12 +152,13 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
     const int hd = p.hd, per_g = (p.r + 2) * hd;
     const int g = n / per_g, rem = n - g * per_g, h = rem / hd, d = rem - h * hd;
     if (h <= p.r) {  // q heads and the k head: rotate pairs (d, d+1), (d+2, d+3)
-      const int64_t pos = p.pos[(int64_t)m * p.pos_sb];
+      const int64_t pos = pre ? 0 : p.pos[(int64_t)m * p.pos_sb];
       const float* cr = p.cos + pos * (hd / 2) + d / 2;
       const float* sr = p.sin + pos * (hd / 2) + d / 2;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float x0 = (float)o[2 * j], x1 = (float)o[2 * j + 1], c = cr[j], sn = sr[j];
+        const float x0 = (float)o[2 * j], x1 = (float)o[2 * j + 1];
+        const float c = pre ? pre->c[j] : cr[j], sn = pre ? pre->s[j] : sr[j];
         o[2 * j] = (T)(x0 * c - x1 * sn);
         o[2 * j + 1] = (T)(x0 * sn + x1 * c);
       }
@@ -125,7 +167,7 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
     if (h < p.r) {
       dst = y + (int64_t)m * p.ldy + (int64_t)(g * p.r + h) * hd + d;
     } else {
-      const int64_t slot = p.slot_ptr ? *p.slot_ptr : p.slot;
+      const int64_t slot = pre ? pre->slot : p.slot_ptr ? *p.slot_ptr : p.slot;
       T* cache = (T*)(h == p.r ? p.kcache : p.vcache);
       dst = cache + slot * p.c_ss + (int64_t)m * p.c_sb + (int64_t)g * hd + d;
     }
@@ -289,8 +331,10 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
   constexpr int WAVES = 8;
   static_assert(STEPS % U == 0, "ring must tile the k-steps");
+  static_assert(!NORM || STEPS == 16, "the normed forms keep 64 gamma chunks per wave");
   __shared__ f4 part[2][WAVES][64];
   __shared__ float ssq[WAVES][16];
+  __shared__ x8 gsh[NORM ? WAVES : 1][64];  // NORM: each wave's gamma slice
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = p.M, N = p.N, K = p.K;
   const T* __restrict__ x = (const T*)p.x;
@@ -306,30 +350,44 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   // round's time halves (Llama-2-7B fc1: 1376 blocks = 5 x 256 + 96 ->
   // at most 5.5 instead of 6 block times per workgroup).  A half block's MFMA
   // rows r and r + 4 read the same W row (one HBM fetch per cache line).
+  // PACKED: the nrem tail blocks are stored as half units (skinny_glu_half_tail;
+  // ops/decode_pack.py): per (half, wave, k-step) 512 contiguous bytes holding
+  // the 4 up + 4 gate rows, which MFMA rows r and r + 4 both read.
   const int nrem = nblocks % G;
-  // (not with PACKED: a half block's 8 W rows are spread over the whole packed
-  // 1 KiB pieces of its 16-row block, so it would stream the full block)
-  const bool halves = EPI == EPI_GLU && !PACKED && nrem > 0 && 2 * nrem <= G && !p.no_halves;
+  const bool halves = EPI == EPI_GLU && nrem > 0 && 2 * nrem <= G;
   const int rounds = halves ? (nblocks - nrem) / G : 0;
   const int nunits = halves ? rounds + (wg < 2 * nrem ? 1 : 0) : (nblocks - wg + G - 1) / G;
   auto unit_blk = [&](int j) { return j < rounds || !halves ? wg + j * G : nblocks - nrem + wg / 2; };
   auto unit_half = [&](int j) { return j < rounds || !halves ? -1 : (wg & 1); };
-  constexpr int WS = PACKED ? 512 : 32;  // elements between a lane's k-steps
+  // elements between a lane's consecutive k-steps of unit j
+  auto wstr = [&](int j) { return !PACKED ? 32 : unit_half(j) < 0 ? 512 : 256; };
   auto wptr = [&](int j) {
     const int b = unit_blk(j), h = unit_half(j);
-    if constexpr (PACKED) return w + ((int64_t)b * WAVES + wave) * STEPS * 512 + 8 * lane;
+    if constexpr (PACKED) {
+      if (h < 0) return w + ((int64_t)b * WAVES + wave) * STEPS * 512 + 8 * lane;
+      const int64_t tail = (int64_t)(nblocks - nrem) * 16 * K;  // full blocks first
+      const int unit = (b - (nblocks - nrem)) * 2 + h, pr = (r & 3) + 4 * (r >> 3);
+      return w + tail + ((int64_t)unit * WAVES + wave) * STEPS * 256 + 8 * (kc + pr);
+    }
     int64_t row;
     if (h < 0) row = w_row<EPI>(b, r, N);
     else row = (r < 8 ? 0 : (int64_t)N) + (int64_t)b * 8 + 4 * h + (r & 3);
     return w + row * K + kbeg + kc;
   };
   int j = 0, blk = unit_blk(0), half = unit_half(0);
+  EpiPre<T, EPI> pre;  // wave 0: the epilogue operands of the current block
+  if (wave == 0) {
+    epi_init<T, EPI>(p, lane, pre);
+    epi_prefetch<T, EPI>(p, blk, lane, pre);
+  }
   const T* wr = wptr(0);
   const T* wn = wptr(nunits > 1 ? 1 : 0);
+  int ws = wstr(0), wsn = wstr(nunits > 1 ? 1 : 0);
 
-  x8 a[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * u));
+  // X (and gamma) first, the weight ring right behind them: a wave's loads
+  // return in order, so X lands first and the norm prologue runs while the
+  // ring's weight loads are in flight (issued the other way round, X came
+  // back only after the whole ring and the first MFMA waited for the norm)
   x8 xs[STEPS];
   {
     const T* xr = x + (int64_t)r * K + kbeg + kc;
@@ -341,8 +399,16 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
       for (int s = 0; s < STEPS; ++s) xs[s] = x8{};
     }
   }
+  // gamma: the wave's K slice is 64 chunks of 8, one 16-B load per lane,
+  // staged through LDS (the per-step fragments would cost 2 x STEPS live
+  // registers; loading them after the norm reduction cost two more round trips)
+  x8 gl{};
+  if constexpr (NORM) gl = *reinterpret_cast<const x8*>((const T*)p.norm_w + kbeg + 8 * lane);
+  __builtin_amdgcn_sched_barrier(0);
+  x8 a[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + ws * u));
   if constexpr (NORM) {
-    const T* gr = (const T*)p.norm_w + kbeg + kc;
     float ss = 0.f;
 #pragma unroll
     for (int s = 0; s < STEPS; ++s)
@@ -354,28 +420,22 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
     if (lane < 16) ssq[wave][lane] = ss;
+    gsh[wave][lane] = gl;
     __syncthreads();
     float tot = 0.f;
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
     const float rs = rsqrtf(tot / (float)K + p.eps);
-    // rounded like rmsnorm_fwd_k; gamma in chunks of 8 fragments (all STEPS
-    // at once would hold 2 x STEPS fragments live and spill at STEPS = 32)
+    // rounded like rmsnorm_fwd_k; step s, lane group q reads chunk 4 s + q
 #pragma unroll
-    for (int s0 = 0; s0 < STEPS; s0 += 8) {
-      x8 g[8];
+    for (int s = 0; s < STEPS; ++s) {
+      const x8 g = gsh[wave][4 * s + (lane >> 4)];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + i));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const T xn = (T)((float)xs[s0 + i][e] * rs);
-          xs[s0 + i][e] = (T)((float)xn * (float)g[i][e]);
-        }
-        if (!xon) xs[s0 + i] = x8{};
+      for (int e = 0; e < 8; ++e) {
+        const T xn = (T)((float)xs[s][e] * rs);
+        xs[s][e] = (T)((float)xn * (float)g[e]);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if (!xon) xs[s] = x8{};
     }
   }
 
@@ -389,7 +449,7 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
     for (int s = 0; s < STEPS; ++s) {
       acc = mfma16x16x32<T>(a[s % U], xs[s], acc);
       if (!LAST || s + U < STEPS) {
-        const T* src = s + U < STEPS ? wr + WS * (s + U) : wn + WS * (s + U - STEPS);
+        const T* src = s + U < STEPS ? wr + ws * (s + U) : wn + wsn * (s + U - STEPS);
         a[s % U] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(src));
       }
       __builtin_amdgcn_sched_barrier(0);  // {MFMA s, refill s} in program order
@@ -405,13 +465,16 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
       f4 t = part[j & 1][0][lane];
 #pragma unroll
       for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][lane];  // fixed order
-      epilogue<T, EPI, ACT>(p, blk, t, lane, half);
+      epilogue<T, EPI, ACT>(p, blk, t, lane, half, &pre);
     }
     if (last) break;
     blk = unit_blk(j + 1);
     half = unit_half(j + 1);
+    if (wave == 0) epi_prefetch<T, EPI>(p, blk, lane, pre);  // lands during the block's k-loop
     wr = wn;
+    ws = wsn;
     wn = wptr(j + 2 < nunits ? j + 2 : nunits - 1);
+    wsn = wstr(j + 2 < nunits ? j + 2 : nunits - 1);
   }
 }
 
@@ -443,13 +506,15 @@ void launch(const SkinnyArgs& p, hipStream_t s) {
                        dim3(64 * WAVES), 0, s, p);
   } else {
     // ring depth (k-steps of weight loads in flight per wave): 16 (batch-1 graph decode
-    // 301 -> 308 tok/s over 8, profiles/r3s_skinny_ring_depth.txt)
+    // 301 -> 308 tok/s over 8, profiles/r3s_skinny_ring_depth.txt); 8 beside the 32
+    // register-resident X fragments of K = 8192 (16 spilled 92-204 B per lane)
+    constexpr int U = STEPS == 32 ? 8 : 16;
     const int g = nblocks < num_cus() ? nblocks : num_cus();
     if (p.packed)
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16, true>), dim3((unsigned)g),
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, true>), dim3((unsigned)g),
                          dim3(512), 0, s, p);
     else
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 16, false>), dim3((unsigned)g),
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, false>), dim3((unsigned)g),
                          dim3(512), 0, s, p);
   }
 }
@@ -498,13 +563,7 @@ bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
 // K = 4096 / 8192 (16 / 32 k-steps per wave) take the persistent form
 // (EMA_SKINNY_PERSIST=0: the one-block-per-workgroup kernel everywhere).
 void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
-  // EMA_SKINNY_HALVES=0: no half-block last round for the GLU (A/B)
-  static const int no_halves = [] {
-    const char* e = getenv("EMA_SKINNY_HALVES");
-    return e && e[0] == '0' ? 1 : 0;
-  }();
   SkinnyArgs p = p0;
-  p.no_halves = no_halves;
   static const int want = [] {
     const char* e = getenv("EMA_SKINNY_WAVES");
     return e ? atoi(e) : 8;
@@ -523,6 +582,22 @@ void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
   }
   if (dt == DT_BF16) w8 ? dispatch<bf16, 8, 0>(p, epi, s) : dispatch<bf16, 4, 0>(p, epi, s);
   else w8 ? dispatch<fp16, 8, 0>(p, epi, s) : dispatch<fp16, 4, 0>(p, epi, s);
+}
+
+// GLU blocks of 8 features (F / 8) the persistent kernel runs as half units
+// in its last round (0: none / not the persistent form).  The decode-packed
+// GLU weight stores exactly these tail blocks in the half-unit layout.
+int skinny_glu_half_tail(int64_t F, int64_t K, bool norm) {
+  static const bool persist = [] {
+    const char* e = getenv("EMA_SKINNY_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  if (K % 256 != 0 || F % 8 != 0) return 0;
+  const int64_t steps = K / 256;
+  if (!persist || !(steps == 16 || (steps == 32 && !norm))) return 0;
+  const int64_t nblocks = F / 8, G = nblocks < num_cus() ? nblocks : num_cus();
+  const int64_t nrem = nblocks % G;
+  return nrem > 0 && 2 * nrem <= G ? (int)nrem : 0;
 }
 
 void skinny_gemm(const void* x, const void* w, void* y, int64_t M, int64_t N, int64_t K, int dt,

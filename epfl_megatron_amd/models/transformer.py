@@ -300,7 +300,7 @@ class ParallelAttention(MegatronModule):
             ctx = self._inference_forward(mixed, attention_mask, inference_params, position_ids,
                                           rope)
         elif self.cp_group is not None:
-            ctx = self._context_parallel_forward(mixed, position_ids, rope)
+            ctx = self._context_parallel_forward(mixed, position_ids, rope, attention_mask)
         elif self.use_flash_attn:
             rng = tp.get_cuda_rng_tracker().fork() if not self.sequence_parallel else nullcontext()
             with rng:
@@ -319,10 +319,12 @@ class ParallelAttention(MegatronModule):
             ctx = self._core(q, self._expand_kv(k), self._expand_kv(v), attention_mask)
         return self.dense(ctx)
 
-    def _context_parallel_forward(self, mixed, position_ids, rope):
+    def _context_parallel_forward(self, mixed, position_ids, rope, attention_mask=None):
         """Causal self-attention of this rank's zig-zag share of the sequence
         over the whole sequence: RoPE at the share's global positions, then the
-        K/V ring (``parallel/context.py``) with the FlashAttention pair kernels."""
+        K/V ring (``parallel/context.py``) with the FlashAttention pair kernels.
+        ``attention_mask``: None, or (``--reset_attention_mask``) the WHOLE
+        sequence's int32 [2, b, S] document bounds."""
         sq, b = mixed.shape[:2]
         if rope is not None:
             if position_ids is None:
@@ -332,8 +334,10 @@ class ParallelAttention(MegatronModule):
             mixed = rope_qkv(mixed.view(sq, b, g, r + 2, hd), rope[0], rope[1],
                              position_ids.long()).view(sq, b, -1)
         q, k, v = self._split_qkv(mixed)
+        docs = attention_mask if (attention_mask is not None and
+                                  attention_mask.dtype == torch.int32) else None
         o = ring_attention(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1),
-                           self.cp_group, causal=True, zigzag=True)
+                           self.cp_group, causal=True, zigzag=True, docs=docs)
         return o.transpose(0, 1).reshape(sq, b, -1)
 
     def _inference_forward(self, mixed, attention_mask, ip, position_ids, rope):
@@ -516,7 +520,8 @@ class ParallelTransformerLayer(MegatronModule):
         wq, wo = sa.query_key_value.weight, sa.dense.weight
         w1, w2 = mlp.dense_h_to_4h.weight, mlp.dense_4h_to_h.weight
         pq, po = decode_pack.packed(wq), decode_pack.packed(wo)
-        p1, p2 = decode_pack.packed(w1, glu=True), decode_pack.packed(w2)
+        tail = C.skinny_glu_half_tail(w1.shape[0] // 2, w1.shape[1], True)
+        p1, p2 = decode_pack.packed(w1, glu=True, half_tail=tail), decode_pack.packed(w2)
         q = C.skinny_qkv_rope_cache(x, wq if pq is None else pq, ln1.weight, ln1.eps, ng, r, hd,
                                     cos, sin, pos, kc, vc,
                                     ip.device_offset if graph else None, 0 if graph else s0,
@@ -539,7 +544,7 @@ class ParallelTransformerLayer(MegatronModule):
                                 x if first else None, po is not None)
         h2 = tp.reduce_from_tensor_model_parallel_region(h2)
         y = C.skinny_norm_glu(h2, w1 if p1 is None else p1, ln2.weight, ln2.eps,
-                              tp.layers._GLU_KIND[mlp.glu_activation], p1 is not None)
+                              tp.layers._GLU_KIND[mlp.glu_activation], p1 is not None, tail)
         h3 = C.skinny_norm_gemm(y, w2 if p2 is None else p2, None, 0.0, h2 if first else None,
                                 p2 is not None)
         h3 = tp.reduce_from_tensor_model_parallel_region(h3)

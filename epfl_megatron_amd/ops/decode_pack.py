@@ -15,7 +15,12 @@ feeds are unchanged, and the stream reaches 4.6-6.0 TB/s
 Layout (K % 256 == 0, S = K / 256 k-steps of 32 per wave, 8 waves):
 ``packed[b, wave, s, q, r, e] = W[row(b, r), wave * 32 S + 32 s + 8 q + e]``
 with ``row(b, r) = 16 b + r`` (plain / QKV) or, for a GLU weight ``[2F, K]``,
-``8 b + r`` (up) / ``F + 8 b + r - 8`` (gate) — the kernel's ``w_row``.
+``8 b + r`` (up) / ``F + 8 b + r - 8`` (gate) — the kernel's ``w_row``.  The
+last ``half_tail`` GLU blocks (``skinny_glu_half_tail``: the persistent
+kernel's last round, run as twice as many 4-feature half units) follow as half
+units ``[unit, wave, s, q, pr, e]`` (512 B per k-step) with ``pr`` = the 4 up
+then the 4 gate rows of features ``8 b + 4 h .. + 3``; MFMA rows r and r + 4
+of a half unit read the same bytes.
 
 The packed copy lives next to the parameter (``_ema_decode_packed``) and is
 rebuilt when the parameter's storage or in-place version changes, i.e. after
@@ -36,9 +41,10 @@ def packable(w):
             and w.dtype in (torch.bfloat16, torch.float16))
 
 
-def pack(w, glu=False):
+def pack(w, glu=False, half_tail=0):
     """The packed copy of ``w`` ([N, K] -> [N, K], same dtype / device)."""
     assert packable(w), f"skinny pack: unsupported weight {tuple(w.shape)} {w.dtype}"
+    assert glu or not half_tail
     n, k = w.shape
     s = k // 256
     if glu:
@@ -48,32 +54,47 @@ def pack(w, glu=False):
     else:
         blocks = w.reshape(n // 16, 16, k)
     nb = blocks.shape[0]
+    full = nb - half_tail
     # [b, r, wave, s, q, e] -> [b, wave, s, q, r, e]: lane q * 16 + r
-    return blocks.reshape(nb, 16, 8, s, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous().reshape(n, k)
+    out = [blocks[:full].reshape(full, 16, 8, s, 4, 8).permute(0, 2, 3, 4, 1, 5).reshape(-1)]
+    if half_tail:
+        t = blocks[full:].reshape(half_tail, 2, 2, 4, k)  # [b, up|gate, h, row, k]
+        t = t.permute(0, 2, 1, 3, 4).reshape(half_tail, 2, 8, 8, s, 4, 8)  # [b, h, pr, ...]
+        # [b, h, pr, wave, s, q, e] -> [b, h, wave, s, q, pr, e]
+        out.append(t.permute(0, 1, 3, 4, 5, 2, 6).reshape(-1))
+    return torch.cat(out).reshape(n, k) if half_tail else out[0].reshape(n, k)
 
 
-def unpack(p, glu=False):
+def unpack(p, glu=False, half_tail=0):
     """Inverse of ``pack`` (tests)."""
     n, k = p.shape
     s = k // 256
     nb = n // 16
-    blocks = p.reshape(nb, 8, s, 4, 16, 8).permute(0, 4, 1, 2, 3, 5).reshape(nb, 16, k)
+    full = nb - half_tail
+    flat = p.reshape(-1)
+    blocks = flat[:full * 16 * k].reshape(full, 8, s, 4, 16, 8).permute(0, 4, 1, 2, 3, 5)
+    blocks = [blocks.reshape(full, 16, k)]
+    if half_tail:
+        t = flat[full * 16 * k:].reshape(half_tail, 2, 8, s, 4, 8, 8).permute(0, 1, 5, 2, 3, 4, 6)
+        t = t.reshape(half_tail, 2, 2, 4, k).permute(0, 2, 1, 3, 4)  # [b, up|gate, h, row, k]
+        blocks.append(t.reshape(half_tail, 16, k))
+    blocks = torch.cat(blocks)
     if glu:
         f = n // 2
         return torch.cat((blocks[:, :8].reshape(f, k), blocks[:, 8:].reshape(f, k)), 0)
     return blocks.reshape(n, k)
 
 
-def packed(w, glu=False):
+def packed(w, glu=False, half_tail=0):
     """Cached packed copy of parameter ``w``, or None when the row-major
     weight must be streamed (disabled / unsupported shape)."""
     if not ENABLED or not packable(w):
         return None
-    key = (w.data_ptr(), w._version, bool(glu), w.dtype, tuple(w.shape))
+    key = (w.data_ptr(), w._version, bool(glu), int(half_tail), w.dtype, tuple(w.shape))
     hit = getattr(w, "_ema_decode_packed", None)
     if hit is not None and hit[0] == key:
         return hit[1]
     with torch.no_grad():
-        p = pack(w.detach(), glu)
+        p = pack(w.detach(), glu, half_tail)
     w._ema_decode_packed = (key, p)
     return p

@@ -16,7 +16,7 @@ from epfl_megatron_amd.models import FalconModel, GPTModel, LlamaModel, ModelTyp
 from epfl_megatron_amd.parallel import tensor as tensor_parallel
 from epfl_megatron_amd.parallel.context import cp_token_mean, get_batch_on_this_cp_rank
 from epfl_megatron_amd.training import pretrain
-from epfl_megatron_amd.utils.misc import (average_losses_across_data_parallel_group,
+from epfl_megatron_amd.utils.misc import (average_losses_across_data_parallel_group, doc_bounds,
                                           get_ltor_masks_and_position_ids)
 
 
@@ -55,10 +55,12 @@ def get_batch(data_iterator):
         tokens, tokenizer.eod, args.reset_position_ids, args.reset_attention_mask,
         args.eod_mask_loss, flash_doc_bounds=args.use_flash_attn)
     if args.context_parallel_size > 1:
-        # this rank's sequence chunk; the causal mask is implied by the ring
+        # this rank's sequence chunk; the causal mask is implied by the ring,
+        # packed documents travel as the WHOLE sequence's int32 [2, b, S] bounds
         tokens, labels, loss_mask, position_ids = get_batch_on_this_cp_rank(
             [tokens, labels, loss_mask, position_ids])
-        attention_mask = None
+        attention_mask = doc_bounds(data_b["text"].long()[:, :-1], tokenizer.eod) \
+            if args.reset_attention_mask else None
     return tokens, labels, loss_mask, attention_mask, position_ids
 
 

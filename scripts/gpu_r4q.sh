@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4q: packed GLU half-unit tail + decode attention with adaptive chunks and in-kernel combine:
+# tests, serving, b1 profile.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_gpu.py tests/test_gpu_e2e.py -m gpu -k "skinny or decode or graph or kvcache or generat" \
+  > gpurun_out/r4q_tests.log 2>&1 || { tail -40 gpurun_out/r4q_tests.log; exit 1; }
+tail -1 gpurun_out/r4q_tests.log
+timeout -k 10 400 python -u scripts/serve_bench.py --batches 1,8,16,32 --graph > gpurun_out/r4q_serve_graph.log 2>&1 || { tail -30 gpurun_out/r4q_serve_graph.log; exit 1; }
+grep '^{"batch' gpurun_out/r4q_serve_graph.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4q_prof_b1 -o s -- python3 scripts/serve_bench.py --batches 1 --graph --gen 64 > gpurun_out/r4q_prof_b1.log 2>&1 || { tail -20 gpurun_out/r4q_prof_b1.log; exit 1; }
+f=$(find gpurun_out/r4q_prof_b1 -name '*kernel_stats.csv' | head -1) && python3 scripts/summarize_prof.py "$f" gpurun_out/r4q_decode_b1_kernels.txt "Llama-2-7B graph decode batch 1 (prompt 128, 64 generated), packed weights + GLU half-unit tail, split decode attention with in-kernel combine" && head -14 gpurun_out/r4q_decode_b1_kernels.txt

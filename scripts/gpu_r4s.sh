@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 4s: decode attention lane-key scores for 4-8 heads per workgroup, skinny gamma via LDS + K=8192 ring 8:
+# prefetch: tests, kpw microbench (+ rocprof), serving, b1 profile.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_gpu.py tests/test_gpu_e2e.py -m gpu -k "skinny or decode or graph or kvcache or generat" \
+  > gpurun_out/r4s_tests.log 2>&1 || { tail -40 gpurun_out/r4s_tests.log; exit 1; }
+tail -1 gpurun_out/r4s_tests.log
+timeout -k 10 200 python -u scripts/decode_kpw_bench.py > gpurun_out/r4s_kpw.txt 2>&1 || { tail -30 gpurun_out/r4s_kpw.txt; exit 1; }
+cat gpurun_out/r4s_kpw.txt
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4s_prof_kpw -o s -- python3 scripts/decode_kpw_bench.py > gpurun_out/r4s_prof_kpw.log 2>&1 || { tail -20 gpurun_out/r4s_prof_kpw.log; exit 1; }
+f=$(find gpurun_out/r4s_prof_kpw -name '*kernel_stats.csv' | head -1) && python3 scripts/summarize_prof.py "$f" gpurun_out/r4s_kpw_kernels.txt "decode attention kpw A/B (scripts/decode_kpw_bench.py)" && head -30 gpurun_out/r4s_kpw_kernels.txt
+timeout -k 10 400 python -u scripts/serve_bench.py --batches 1,8,16,32 --graph > gpurun_out/r4s_serve_graph.log 2>&1 || { tail -30 gpurun_out/r4s_serve_graph.log; exit 1; }
+grep '^{"batch' gpurun_out/r4s_serve_graph.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4s_prof_b1 -o s -- python3 scripts/serve_bench.py --batches 1 --graph --gen 64 > gpurun_out/r4s_prof_b1.log 2>&1 || { tail -20 gpurun_out/r4s_prof_b1.log; exit 1; }
+f=$(find gpurun_out/r4s_prof_b1 -name '*kernel_stats.csv' | head -1) && python3 scripts/summarize_prof.py "$f" gpurun_out/r4s_decode_b1_kernels.txt "Llama-2-7B graph decode batch 1 (prompt 128, 64 generated): packed weights, GLU half tail, epilogue prefetch, decode attention auto kpw" && head -14 gpurun_out/r4s_decode_b1_kernels.txt

@@ -91,3 +91,64 @@ def test_ring_attention_simulated_matches_full(zigzag):
         for i in range(W):
             torch.testing.assert_close(got[i].float(), _share(want, i, W, zigzag),
                                        atol=5e-5, rtol=5e-5)
+
+
+def _docs(b, s, seed):
+    """Packed-document bounds of random token rows with EOD (token 0) at a
+    few random positions: documents cross the chunk / piece boundaries."""
+    from epfl_megatron_amd.utils.misc import doc_bounds
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(1, 50, (b, s), generator=g)
+    for i in range(b):
+        for p in torch.randperm(s - 1, generator=g)[: 2 + i]:
+            tok[i, p] = 0
+    return doc_bounds(tok, 0)
+
+
+def _ring_docs_rank(rank, world, nq, nkv, zigzag):
+    import torch.distributed as dist
+    from epfl_megatron_amd.parallel.context import ring_attention
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, s, d = 2, 12 * world, 16
+    q, k, v, go = _full(b, s, nq, nkv, d, seed=7)
+    docs = _docs(b, s, seed=11)
+    ql, kl, vl = (_share(t, rank, world, zigzag).clone().requires_grad_() for t in (q, k, v))
+    out = ring_attention(ql, kl, vl, dist.group.WORLD, causal=True, zigzag=zigzag, docs=docs)
+    out.backward(_share(go, rank, world, zigzag))
+    return out.detach(), ql.grad, kl.grad, vl.grad
+
+
+@pytest.mark.parametrize("world,nq,nkv,zigzag", [(2, 4, 4, False), (2, 4, 2, True),
+                                                 (4, 4, 2, True), (3, 6, 2, True)])
+def test_ring_attention_document_masks(world, nq, nkv, zigzag):
+    """--reset_attention_mask under context parallelism: the ring with the
+    whole sequence's document bounds equals full-sequence document-masked
+    attention (outputs and dQ / dK / dV of every rank's share)."""
+    from epfl_megatron_amd.ops.attention import attention_ref
+    res = run_dist(_ring_docs_rank, world, nq, nkv, zigzag)
+    b, s, d = 2, 12 * world, 16
+    q, k, v, go = _full(b, s, nq, nkv, d, seed=7)
+    docs = _docs(b, s, seed=11)
+    qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
+    ref = attention_ref(qr, kr, vr, causal=True, doc_bounds=docs)
+    ref.backward(go)
+    for rank, (o, dq, dk, dv) in enumerate(res):
+        sh = lambda t: _share(t, rank, world, zigzag)  # noqa: E731
+        torch.testing.assert_close(o, sh(ref.detach()), atol=2e-5, rtol=2e-5)
+        torch.testing.assert_close(dq, sh(qr.grad), atol=5e-5, rtol=5e-5)
+        torch.testing.assert_close(dk, sh(kr.grad), atol=5e-5, rtol=5e-5)
+        torch.testing.assert_close(dv, sh(vr.grad), atol=5e-5, rtol=5e-5)
+
+
+def test_ring_document_pair_arrays():
+    """Per-pair local document arrays: first local key at / after each query's
+    document start, first local query at / after each key's document end."""
+    from epfl_megatron_amd.parallel.context import _pair_docs
+    docs = torch.tensor([[[0, 0, 0, 3, 3, 3, 3, 7, 7, 7]], [[3, 3, 3, 7, 7, 7, 7, 10, 10, 10]]],
+                        dtype=torch.int32)
+    pq, pk = torch.tensor([6, 7, 8, 9]), torch.tensor([1, 2, 3, 4])
+    pd = _pair_docs(docs, pq, pk)
+    # q 6 (doc [3, 7)) -> first key >= 3 is local 2; q 7..9 (doc [7, 10)) -> 4 (none)
+    assert pd[0, 0].tolist() == [2, 4, 4, 4]
+    # key 1, 2 end at 3 -> first query >= 3 is local 0; keys 3, 4 end at 7 -> local 1
+    assert pd[1, 0].tolist() == [0, 0, 1, 1]

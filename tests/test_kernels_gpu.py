@@ -570,13 +570,14 @@ def test_skinny_fused_qkv_rope_cache(ng, r, hd, graph_slot):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 12288, 4096), (16, 4096, 11008),
-                                   (3, 1024, 8192), (5, 512, 512)])
+                                   (3, 1024, 8192), (5, 512, 512), (1, 22016, 4096)])
 def test_skinny_packed_weights_match_row_major(M, N, K):
     """The decode-packed weight layout (ops/decode_pack.py) feeds every lane
     the same k indices in the same order as the row-major stream: plain,
     norm + residual, norm + GLU and QKV + RoPE + cache outputs are bit-equal
     across the persistent (K = 4096 / 8192) and per-block (K = 11008 / 512)
-    forms."""
+    forms; N = 22016 is Llama-2-7B's fc1, whose last round runs as half units
+    (1376 blocks = 5 x 256 + 96 on 256 CUs) from the packed half-unit tail."""
     from epfl_megatron_amd.ops import decode_pack
     from epfl_megatron_amd.ops.rope import rope_table
     C = _ext()
@@ -591,8 +592,11 @@ def test_skinny_packed_weights_match_row_major(M, N, K):
         assert torch.equal(C.skinny_gemm(x, wp, True), C.skinny_gemm(x, w))
         assert torch.equal(C.skinny_norm_gemm(x, wp, g, 1e-5, res, True),
                            C.skinny_norm_gemm(x, w, g, 1e-5, res))
+        tail = C.skinny_glu_half_tail(N // 2, K, True)
+        wg = decode_pack.pack(w, glu=True, half_tail=tail)
+        assert torch.equal(decode_pack.unpack(wg, glu=True, half_tail=tail), w)
         for kind in (0, 1):
-            assert torch.equal(C.skinny_norm_glu(x, decode_pack.pack(w, glu=True), g, 1e-6, kind, True),
+            assert torch.equal(C.skinny_norm_glu(x, wg, g, 1e-6, kind, True, tail),
                                C.skinny_norm_glu(x, w, g, 1e-6, kind)), kind
         hd = 128
         if N % (3 * hd) == 0:
@@ -894,6 +898,43 @@ def test_ring_attention_kernels(W, causal, nq, nkv, hd, zigzag):
                                  (dks, kr.grad, 6e-2, "dk"), (dvs, vr.grad, 6e-2, "dv")):
         _close(torch.cat(got, 1), torch.cat([share(want, i) for i in range(W)], 1), tol, tol,
                f"ring {name}")
+
+
+@pytest.mark.parametrize("W,nq,nkv,hd,zigzag", [(4, 8, 2, 128, True), (2, 4, 4, 64, False),
+                                                  (3, 6, 1, 128, True)])
+def test_ring_attention_kernels_document_masks(W, nq, nkv, hd, zigzag):
+    """Context parallelism with packed documents (--reset_attention_mask): the
+    pair kernels take per-pair local document arrays, off-diagonal pairs run
+    the causal kernel with offset sk (document starts only) and split into
+    square quarters; vs the fp32 full-sequence document-masked reference.
+    Some rows of an off-diagonal pair see no key (their document starts after
+    the K chunk): LSE -inf, merged away."""
+    from epfl_megatron_amd.ops.attention import attention_ref
+    from epfl_megatron_amd.parallel.context import ring_attention_simulated, zigzag_slice
+    from epfl_megatron_amd.utils.misc import doc_bounds
+    torch.manual_seed(W * 100 + hd)
+    b, c = 2, 192
+    s = W * c
+    tok = torch.randint(1, 100, (b, s))
+    for i in range(b):
+        tok[i, torch.randperm(s - 1)[:3 + 2 * i]] = 0
+    docs = doc_bounds(tok, 0).to(DEV)
+    q = torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(b, s, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(b, s, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    go = torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16)
+    share = (lambda t, i: zigzag_slice(t, 1, i, W)) if zigzag else \
+        (lambda t, i: t[:, i * c:(i + 1) * c])  # noqa: E731
+    ch = lambda t: [share(t, i).contiguous() for i in range(W)]  # noqa: E731
+    outs, (dqs, dks, dvs) = ring_attention_simulated(ch(q), ch(k), ch(v), True, grad_outs=ch(go),
+                                                     zigzag=zigzag, docs=docs)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = attention_ref(qr, kr, vr, causal=True, doc_bounds=docs)
+    ref.backward(go.float())
+    for got, want, tol, name in ((outs, ref.detach(), 2e-2, "fwd"), (dqs, qr.grad, 6e-2, "dq"),
+                                 (dks, kr.grad, 6e-2, "dk"), (dvs, vr.grad, 6e-2, "dv")):
+        _close(torch.cat(got, 1), torch.cat([share(want, i) for i in range(W)], 1), tol, tol,
+               f"ring docs {name}")
 
 
 @pytest.mark.gpu

@@ -370,3 +370,17 @@ def test_llama_cp_tp_dp_pp():
     got = _losses(run_dist(_train, 4, argv + ["--pipeline_model_parallel_size", "2",
                                               "--context_parallel_size", "2"], 2))
     _check(base, got, tol=5e-5)
+
+
+def test_llama_context_parallel_document_masks():
+    """--reset_attention_mask / --reset_position_ids (packed documents) under
+    context parallelism: the ring masks earlier documents from the whole
+    sequence's bounds; CP 2 and CP 4 train like CP 1.  A vocabulary of 8
+    makes EOD (token 7) frequent, so documents cross the zig-zag pieces."""
+    argv = [("8" if a == "250" else a) for a in TINY_LLAMA] + [
+        "--reset_attention_mask", "--reset_position_ids",
+        "--micro_batch_size", "2", "--global_batch_size", "4"]
+    base = _losses(run_dist(_train, 1, argv, 3))
+    for cp in (2, 4):
+        got = _losses(run_dist(_train, cp, argv + ["--context_parallel_size", str(cp)], 3))
+        _check(base, got)

@@ -452,5 +452,15 @@ def test_decode_pack_layout():
         for (b, wv, s, q, r, e) in [(0, 0, 0, 0, 0, 0), (1, 3, 1, 2, 9, 5), (3, 7, 1, 3, 15, 7)]:
             row = (8 * b + r if r < 8 else 32 + 8 * b + r - 8) if glu else 16 * b + r
             assert pv[b, wv, s, q, r, e] == w[row, wv * 32 * S + 32 * s + 8 * q + e]
+    # GLU half-unit tail: [unit, wave, s, q, pr, e], pr = 4 up then 4 gate rows
+    F = 56
+    w = torch.randn(2 * F, 256 * S).bfloat16()
+    p = dp.pack(w, True, half_tail=3)
+    assert torch.equal(dp.unpack(p, True, half_tail=3), w)
+    full = F // 8 - 3
+    v = p.reshape(-1)[full * 16 * 256 * S:].view(3, 2, 8, S, 4, 8, 8)
+    for (bt, h, wv, s, q, pr, e) in [(0, 0, 0, 0, 0, 0, 0), (2, 1, 7, 1, 3, 7, 5), (1, 0, 3, 1, 2, 5, 1)]:
+        f = 8 * (full + bt) + 4 * h + (pr & 3)
+        assert v[bt, h, wv, s, q, pr, e] == w[f if pr < 4 else F + f, wv * 32 * S + 32 * s + 8 * q + e]
     assert not dp.packable(torch.zeros(16, 384).bfloat16())
     assert not dp.packable(torch.zeros(16, 512))
