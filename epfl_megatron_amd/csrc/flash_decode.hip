@@ -325,21 +325,19 @@ __global__ __launch_bounds__(256) void decode_attn_k(const DecodeParams p) {
   }
 }
 
-// keys per wave: the largest of 64 / 16 / 8 whose grid still covers 256 CUs
-// (1-2 heads per workgroup)
+// keys per wave (1-2 heads per workgroup): 64 when that grid covers the 256
+// CUs, else 16 when its grid covers half of them, else 8
 // (batch-1 MHA at 256 cached keys: 32 heads x 1 chunk of 256 left 224 CUs
-// idle and each busy CU pulling 128 KiB; 8 keys per wave -> 256 workgroups)
+// idle and each busy CU pulling 128 KiB; 16 keys per wave -> 128 workgroups)
 int decode_kpw_auto(int b, int sk, int nq, int nkv) {
   const int r = nq / nkv, rh = r >= 8 ? 8 : r >= 4 ? 4 : r >= 2 ? 2 : 1;
   // 4-8 heads per workgroup score lane = key: fewer keys per wave idle lanes
   // (b = 1 GQA at 3000 keys: 29 us at 64, 53 at 16; profiles/r4s_kpw.txt)
   if (rh >= 4) return 64;
   const int64_t base = (int64_t)b * nkv * ((r + rh - 1) / rh);
-  for (int kpw : {64, 16}) {
-    const int dch = 4 * kpw;
-    if (base * ((sk + dch - 1) / dch) >= 256) return kpw;
-  }
-  return 8;
+  auto grid = [&](int kpw) { return base * ((sk + 4 * kpw - 1) / (4 * kpw)); };
+  if (grid(64) >= 256) return 64;
+  return grid(16) >= 128 ? 16 : 8;  // b = 1 MHA, 256 keys: 16 -> 7.0 us, 8 -> 7.4 (r4t_kpw)
 }
 
 template <typename T, int HD, int RH>
