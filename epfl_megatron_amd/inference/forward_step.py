@@ -57,9 +57,10 @@ class ForwardStep:
         self.threshold = args.inference_batch_times_seqlen_threshold
         self.graphed = None
         if getattr(args, "inference_hip_graph", False):
-            from .hip_graph import GraphedDecodeForward, graph_decode_supported
-            if graph_decode_supported():
-                self.graphed = GraphedDecodeForward(model, self.inference_params, max_batch_size)
+            # a hipGraph per pipeline stage on the GPU; on the CPU the same
+            # static-buffer step runs eagerly
+            from .hip_graph import GraphedDecodeForward
+            self.graphed = GraphedDecodeForward(model, self.inference_params, max_batch_size)
 
     def __call__(self, tokens, position_ids, attention_mask):
         if self.graphed is not None and tokens.size(1) == 1 and \

@@ -30,8 +30,18 @@ communicator is created by the eager warm-up forward, before capture, and the
 collective layer records no timing events while capturing).  All TP ranks run
 the generation loop in lockstep, as the reference's TP generation does
 (``megatron/text_generation/generation.py:179-264``), so every replay issues
-the same collective sequence on every rank.  Pipeline parallelism stays eager
-(a step is a chain of stage-to-stage sends across ranks).
+the same collective sequence on every rank.
+
+Pipeline parallelism (``GraphedDecodeForward``): every stage captures its own
+layers; the stage boundaries stay eager p2p around the replay (the hidden
+state is received into a static buffer the graph reads, the static output is
+sent after the replay), as the reference's PP forward step does
+(``megatron/text_generation/forward_step.py:153-204``).  The launch-bound part
+(tens of small kernels per layer) is in the graph; one send / recv per stage
+per token is not.  ``GraphedGreedyDecoder`` (argmax and the token feedback in
+the graph) needs the whole model on the rank: PP = 1.  Without a GPU the
+same static-buffer step runs eagerly (the CPU / gloo tests drive the PP
+plumbing through it).
 
 The reference decodes eagerly (``megatron/text_generation/generation.py``
 drives ``forward_step.py`` once per token); this is an MI355X-side addition.
@@ -43,15 +53,22 @@ from ..parallel import state
 
 def _check_supported():
     if state.model_parallel_is_initialized() and state.get_pipeline_model_parallel_world_size() > 1:
-        raise NotImplementedError("hipGraph decode runs without pipeline parallelism (PP = 1)")
+        raise NotImplementedError("the graphed greedy loop needs the whole model (PP = 1); "
+                                  "GraphedDecodeForward runs per pipeline stage")
     if not torch.cuda.is_available():
         raise RuntimeError("hipGraph decode needs a GPU")
 
 
 def graph_decode_supported():
-    return torch.cuda.is_available() and (
-        not state.model_parallel_is_initialized()
-        or state.get_pipeline_model_parallel_world_size() == 1)
+    """GraphedDecodeForward captures on a GPU at any TP / PP size."""
+    return torch.cuda.is_available()
+
+
+def _pp_stage():
+    """(first stage, last stage) of this rank (a single stage without PP)."""
+    if not state.model_parallel_is_initialized():
+        return True, True
+    return state.is_pipeline_first_stage(), state.is_pipeline_last_stage()
 
 
 class GraphedDecodeForward:
@@ -62,29 +79,44 @@ class GraphedDecodeForward:
     stay in the (eager) generation loop.  Returns the static logits buffer,
     valid until the next call."""
 
-    def __init__(self, model, inference_params, batch):
-        _check_supported()
+    def __init__(self, model, inference_params, batch, capture=None):
         self.model = model
         self.ip = inference_params
-        dev = torch.device("cuda", torch.cuda.current_device())
+        self.capture = torch.cuda.is_available() if capture is None else capture
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.capture else \
+            torch.device("cpu")
         self.tokens = torch.zeros(batch, 1, dtype=torch.long, device=dev)
         self.pos = torch.zeros(batch, 1, dtype=torch.long, device=dev)
         self.ip.device_offset = torch.zeros(1, dtype=torch.long, device=dev)
         self.ip.device_kv_len = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.first, self.last = _pp_stage()
+        self.recv = None
+        if not self.first:  # static input of this stage's graph: the previous stage's output
+            from .forward_step import _allocate_recv_buffer
+            self.recv = _allocate_recv_buffer(batch, 1)
         self.graph = None
-        self.logits = None
+        self.out = None
 
     def _forward(self):
+        if self.recv is not None:
+            self.model.set_input_tensor(self.recv)
         return self.model(self.tokens, self.pos, None, inference_params=self.ip)
 
     def __call__(self, tokens, position_ids):
+        """One decode step of this stage: the logits on the last stage, None on
+        the others (their output went to the next stage)."""
+        from .communication import recv_from_prev_pipeline_rank_, send_to_next_pipeline_rank
         ip = self.ip
         with torch.no_grad():
             self.tokens.copy_(tokens)
             self.pos.copy_(position_ids)
             ip.device_offset.fill_(ip.sequence_len_offset)
             ip.device_kv_len.fill_(ip.sequence_len_offset + 1)
-            if self.graph is None:
+            if self.recv is not None:
+                recv_from_prev_pipeline_rank_(self.recv)
+            if not self.capture:
+                self.out = self._forward()
+            elif self.graph is None:
                 cur = torch.cuda.current_stream()
                 side = torch.cuda.Stream()
                 side.wait_stream(cur)
@@ -93,9 +125,12 @@ class GraphedDecodeForward:
                 cur.wait_stream(side)
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph):
-                    self.logits = self._forward()
-        self.graph.replay()
-        return self.logits
+                    self.out = self._forward()
+            if self.graph is not None:
+                self.graph.replay()
+            if not self.last:
+                send_to_next_pipeline_rank(self.out)
+        return self.out if self.last else None
 
 
 class GraphedGreedyDecoder:

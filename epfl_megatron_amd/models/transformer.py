@@ -365,7 +365,8 @@ class ParallelAttention(MegatronModule):
         if getattr(ip, "device_offset", None) is not None and sq == 1:
             # hipGraph decode step (inference/hip_graph.py): cache slot and key
             # count live in device tensors, so no launch depends on the step
-            if not (use_native(q) and q.shape[-1] in (64, 128)):
+            # (on the CPU the static-buffer step runs eagerly: reference attention)
+            if q.is_cuda and not (use_native(q) and q.shape[-1] in (64, 128)):
                 raise NotImplementedError("hipGraph decode needs the native decode attention "
                                           "kernel (GPU, bf16/fp16, head_dim 64 or 128)")
             kc, vc = kmem[:, b0:b0 + b], vmem[:, b0:b0 + b]

@@ -90,13 +90,20 @@ def _check_generation(res, ref, n=6):
 
 @pytest.mark.parametrize("extra", [[], ["--inference_hip_graph"]])
 def test_kv_cached_greedy_matches_full_forward(greedy_ref, extra):
-    # without a GPU --inference_hip_graph must fall back to the eager step
+    # without a GPU --inference_hip_graph runs its static-buffer step eagerly
+    # (device slot / key-count tensors, no capture)
     res = run_dist(_generate, 1, extra, 6)[0]
     _check_generation(res, greedy_ref)
 
 
 @pytest.mark.parametrize("extra,world", [(["--tensor_model_parallel_size", "2"], 2),
-                                         (["--pipeline_model_parallel_size", "2"], 2)])
+                                         (["--pipeline_model_parallel_size", "2"], 2),
+                                         # per-stage graphed decode step: static recv
+                                         # buffer in, static output sent after the step
+                                         (["--pipeline_model_parallel_size", "2",
+                                           "--inference_hip_graph"], 2),
+                                         (["--tensor_model_parallel_size", "2",
+                                           "--inference_hip_graph"], 2)])
 def test_parallel_generation_matches(greedy_ref, extra, world):
     res = [r for r in run_dist(_generate, world, extra, 6) if r is not None][0]
     _check_generation(res, greedy_ref)
