@@ -872,6 +872,38 @@ void flash_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   ema::flash_decode(p, dtype_code(q), cur_stream());
 }
 
+// ---------------------------------------------------------------- greedy decode tail
+// logits [b, V] (a view: rows 16-B aligned, last dim contiguous); tokens /
+// pos int64 with b contiguous elements, history int64 [b, H] rows contiguous,
+// step_idx / slot int64 [1], kv_len int32 [1], counter int32 [1] (zeroed once).
+void greedy_tail(const at::Tensor& logits, at::Tensor tokens, at::Tensor history,
+                 at::Tensor step_idx, at::Tensor pos, at::Tensor slot, at::Tensor kv_len,
+                 at::Tensor counter) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "greedy_tail: logits [b, V], V contiguous");
+  const int dt = dtype_code(logits);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16 || dt == ema::DT_F32, "greedy_tail: dtype");
+  const int64_t b = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(b >= 1 && V >= 1 && V < (1ll << 31), "greedy_tail: shape");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0 &&
+                  (logits.stride(0) * logits.element_size()) % 16 == 0,
+              "greedy_tail: logits rows must be 16-byte aligned");
+  for (const at::Tensor* t : {&tokens, &history, &step_idx, &pos, &slot})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong, "greedy_tail: int64 state tensors");
+  TORCH_CHECK(kv_len.is_cuda() && kv_len.scalar_type() == at::kInt && kv_len.numel() >= 1 &&
+                  counter.is_cuda() && counter.scalar_type() == at::kInt && counter.numel() >= 1,
+              "greedy_tail: kv_len / counter int32");
+  TORCH_CHECK(tokens.is_contiguous() && tokens.numel() == b && pos.is_contiguous() &&
+                  pos.numel() == b && history.dim() == 2 && history.size(0) == b &&
+                  history.stride(1) == 1 && step_idx.numel() >= 1 && slot.numel() >= 1,
+              "greedy_tail: tokens / pos [b], history [b, H]");
+  ema::greedy_tail(logits.data_ptr(), logits.stride(0), (int)V, (int)b, dt,
+                   tokens.data_ptr<int64_t>(), history.data_ptr<int64_t>(), history.stride(0),
+                   step_idx.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), slot.data_ptr<int64_t>(),
+                   kv_len.data_ptr<int>(), reinterpret_cast<unsigned*>(counter.data_ptr<int>()),
+                   cur_stream());
+}
+
 // ---------------------------------------------------------------- bias-dropout-add
 at::Tensor bias_dropout_add_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& x2,
                                 const c10::optional<at::Tensor>& bias, const at::Tensor& res,
@@ -1180,6 +1212,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("rope_cos"), py::arg("rope_sin"), py::arg("rope_pos"),
         py::arg("docs"), py::arg("coff") = -1);
   m.def("fa_set_stamps", &fa_set_stamps);
+  m.def("greedy_tail", &greedy_tail);
   m.def("flash_decode", &flash_decode, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"),
         py::arg("b"), py::arg("sk"), py::arg("nq"), py::arg("nkv"), py::arg("hd"), py::arg("qs"),
         py::arg("ks"), py::arg("vs"), py::arg("os"), py::arg("scale"), py::arg("kv_len"),

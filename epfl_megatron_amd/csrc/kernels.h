@@ -198,6 +198,14 @@ struct DecodeParams {
   int kpw;  // keys per wave: 64 / 16 / 8 (flash_decode_kpw picks; chunk = 4 kpw keys)
 };
 int flash_decode_kpw(int b, int sk, int nq, int nkv);
+
+// ---- decode_tail.hip -----------------------------------------------------------------------------
+// Graphed greedy decode step tail: argmax of each row of logits [b, V] (row
+// stride ld) -> tokens[b], history[b, *step_idx], pos[b] += 1; the last
+// workgroup advances *step_idx, *slot and *kv_len (counter: zeroed uint32).
+void greedy_tail(const void* logits, int64_t ld, int V, int b, int dt, int64_t* tokens,
+                 int64_t* history, int64_t hist_ld, int64_t* step_idx, int64_t* pos, int64_t* slot,
+                 int* kv_len, unsigned* counter, hipStream_t s);
 int flash_decode_splits(int sk, int kpw);
 int flash_decode_counters(int b, int nq, int nkv);
 void flash_decode(const DecodeParams& p, int dt, hipStream_t s);

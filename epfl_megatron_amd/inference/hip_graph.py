@@ -159,6 +159,7 @@ class GraphedGreedyDecoder:
         self.history = torch.zeros(batch, max_new_tokens + 1, dtype=torch.long, device=dev)
         self.ip.device_offset = torch.zeros(1, dtype=torch.long, device=dev)
         self.ip.device_kv_len = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tail_counter = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         self.logits = None
         self.steps_done = 0
@@ -168,7 +169,16 @@ class GraphedGreedyDecoder:
 
     def _body(self):
         logits = self._forward()
-        nxt = logits[:, -1].argmax(-1, keepdim=True)
+        last = logits[:, -1]
+        if self._fused_tail(last):
+            # argmax, token / history writes and the four increments in one
+            # launch (csrc/decode_tail.hip; seven launches otherwise)
+            from ..ops._ext import ext
+            ext().greedy_tail(last, self.tokens.view(-1), self.history, self.step_idx,
+                              self.pos.view(-1), self.ip.device_offset, self.ip.device_kv_len,
+                              self.tail_counter)
+            return logits
+        nxt = last.argmax(-1, keepdim=True)
         self.history.index_copy_(1, self.step_idx, nxt)
         self.tokens.copy_(nxt)
         self.pos.add_(1)
@@ -176,6 +186,12 @@ class GraphedGreedyDecoder:
         self.ip.device_offset.add_(1)
         self.ip.device_kv_len.add_(1)
         return logits
+
+    def _fused_tail(self, last):
+        from ..ops._ext import use_native
+        return (use_native(last) and last.dim() == 2 and last.stride(1) == 1
+                and last.dtype in (torch.bfloat16, torch.float16, torch.float32)
+                and last.data_ptr() % 16 == 0 and (last.stride(0) * last.element_size()) % 16 == 0)
 
     def start(self, next_tokens, position):
         """Set the first token to feed (``[batch, 1]``) at absolute ``position``

@@ -979,3 +979,31 @@ def test_rope_qkv_autograd_matches_reference():
     yr.backward(gy.float())
     _close(y, yr, 2e-2, 1e-2, "rope_qkv fwd")
     _close(x.grad, xr.grad, 2e-2, 1e-2, "rope_qkv bwd")
+
+
+@pytest.mark.parametrize("b,V,dtype", [(1, 32000, torch.bfloat16), (5, 1003, torch.bfloat16),
+                                       (3, 32000, torch.float32), (16, 4096, torch.float16)])
+def test_greedy_tail_matches_torch(b, V, dtype):
+    """csrc/decode_tail.hip: per-row argmax (first maximum, as torch.argmax),
+    token / history writes, position increment, and the step / slot / key-count
+    increments by the last workgroup; twice, so the arrival counter re-arms."""
+    C = _ext()
+    torch.manual_seed(b * V)
+    full = torch.randn(b, (V + 5 + 7) // 8 * 8, device=DEV).to(dtype)
+    logits = full[:, :V]  # a strided view, rows 16-B aligned
+    logits[:, V // 3] = logits.max(1).values  # ties: the first index wins
+    tokens = torch.zeros(b, dtype=torch.long, device=DEV)
+    history = torch.full((b, 8), -1, dtype=torch.long, device=DEV)
+    step = torch.tensor([2], dtype=torch.long, device=DEV)
+    pos = torch.arange(b, dtype=torch.long, device=DEV) + 10
+    slot = torch.tensor([40], dtype=torch.long, device=DEV)
+    kvl = torch.tensor([41], dtype=torch.int32, device=DEV)
+    counter = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for it in range(2):
+        C.greedy_tail(logits, tokens, history, step, pos, slot, kvl, counter)
+        want = logits.float().argmax(1)
+        assert torch.equal(tokens, want)
+        assert torch.equal(history[:, 2 + it], want)
+    assert torch.all(history[:, :2] == -1) and torch.all(history[:, 4:] == -1)
+    assert step.item() == 4 and slot.item() == 42 and kvl.item() == 43 and counter.item() == 0
+    assert torch.equal(pos, torch.arange(b, device=DEV) + 12)
