@@ -640,30 +640,73 @@ class _GluMLPFn(torch.autograd.Function):
 # the same pieces, so dW sums pair matching rows.  Collectives of piece j+1 run
 # on RCCL's stream while piece j computes.  Reference (blocking forms):
 # megatron/core/tensor_parallel/layers.py:225-243, mappings.py:107-124, 244-246.
+def _sp_mlp_pieces(rl, world, n_fc1):
+    """Per-rank row counts of the SP MLP pipeline's pieces.
+
+    Even pieces (``EMA_SP_CHUNKS``) unless they quantize the fc1 + GLU GEMM
+    (256 x 256 tiles over the CUs) into more rounds than the monolithic
+    product: Llama-2-7B at TP 8 (16384 rows, 2F = 2752: 11 tile columns) in
+    two 32-tile-row pieces runs 2 + 2 rounds against 3 (pieces / mono 1.255,
+    profiles/r4d_sp_pieces.txt).  Then the first piece takes the largest
+    tile-aligned row count whose tiles fill whole rounds and the second the
+    rest (23 + 41 tile rows: 1 + 2 rounds).  ``EMA_SP_MLP_PIECES=r0,r1,...``
+    forces the split (tests)."""
+    forced = os.environ.get("EMA_SP_MLP_PIECES")
+    if forced:
+        sizes = [int(v) for v in forced.split(",")]
+        if sum(sizes) == rl and all(v > 0 for v in sizes):
+            return sizes
+    c = _sp_pieces(rl)
+    even = [rl // c] * c
+    if c == 1 or not torch.cuda.is_available() or (world * rl) % 256:
+        return even
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    ntile = -(-n_fc1 // 256)
+    mt = world * rl // 256
+
+    def rounds(m):
+        return -(-m * ntile // cus)
+    mono = rounds(mt)
+    if sum(rounds(world * r // 256) for r in even) <= mono or (world * (rl // c)) % 256:
+        return even
+    per_round = cus // ntile
+    for k in range(1, mono):
+        m1 = k * per_round
+        if m1 >= mt:
+            break
+        if rounds(m1) + rounds(mt - m1) <= mono and (m1 * 256) % world == 0:
+            r1 = m1 * 256 // world
+            return [r1, rl - r1]
+    return even
+
+
 def _sp_mlp_forward(x_local, w1, w2, kind):
     world, group = _tp()
     rl, H = x_local.shape
-    c = _sp_pieces(rl)
-    R = rl // c
     dt, dev = x_local.dtype, x_local.device
     F = w2.shape[1]
-    g = get_global_memory_buffer().get_tensor((c, world * R, H), dt, "mpu")
-    works = [comm.all_gather_into(g[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
-             for j in range(c)]
-    pre = torch.empty(c, world * R, 2 * F, dtype=dt, device=dev)
-    y = torch.empty(c, world * R, F, dtype=dt, device=dev)
-    part = torch.empty(c, world * R, w2.shape[0], dtype=dt, device=dev)
+    sizes = _sp_mlp_pieces(rl, world, 2 * F)
+    offs = [sum(sizes[:j]) for j in range(len(sizes))]
+    # piece-major buffers: piece j's gathered rows at [world * off_j, world * (off_j + R_j))
+    g = get_global_memory_buffer().get_tensor((world * rl, H), dt, "mpu")
+    gp = [g[world * o:world * (o + r)] for o, r in zip(offs, sizes)]
+    works = [comm.all_gather_into(gp[j], x_local[o:o + r], group=group, async_op=True)
+             for j, (o, r) in enumerate(zip(offs, sizes))]
+    pre = torch.empty(world * rl, 2 * F, dtype=dt, device=dev)
+    y = torch.empty(world * rl, F, dtype=dt, device=dev)
+    part = torch.empty(world * rl, w2.shape[0], dtype=dt, device=dev)
     out = torch.empty(rl, w2.shape[0], dtype=dt, device=dev)
     rs = []
-    for j in range(c):
+    for j, (o, r) in enumerate(zip(offs, sizes)):
+        rows = slice(world * o, world * (o + r))
         works[j].wait()
-        gemm_glu(g[j], w1, kind, pre[j], y[j])
-        gemm(y[j], w2, part[j])
-        rs.append(comm.reduce_scatter_into(out[j * R:(j + 1) * R], part[j], group=group,
+        gemm_glu(gp[j], w1, kind, pre[rows], y[rows])
+        gemm(y[rows], w2, part[rows])
+        rs.append(comm.reduce_scatter_into(out[o:o + r], part[rows], group=group,
                                            async_op=True))
     for w in rs:
         w.wait()
-    return pre.view(c * world * R, 2 * F), y.view(c * world * R, F), out
+    return pre, y, out
 
 
 def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf):
@@ -676,33 +719,33 @@ def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf):
     if not x_local.is_contiguous():
         x_local = x_local.contiguous()
     rl, H = x_local.shape
-    c = _sp_pieces(rl)
-    R = rl // c
     dt, dev = x_local.dtype, x_local.device
     F = w2.shape[1]
+    sizes = _sp_mlp_pieces(rl, world, 2 * F)
+    offs = [sum(sizes[:j]) for j in range(len(sizes))]
+    pieces = list(zip(offs, sizes))
     buf = get_global_memory_buffer()
-    g2 = buf.get_tensor((c, world * R, g_local.shape[1]), g_local.dtype, "mpu_dy")
-    gw = [comm.all_gather_into(g2[j], g_local[j * R:(j + 1) * R], group=group, async_op=True)
-          for j in range(c)]
-    xt = buf.get_tensor((c, world * R, H), dt, "mpu")
-    xw = [comm.all_gather_into(xt[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
-          for j in range(c)]
-    pre3 = pre.view(c, world * R, 2 * F)
-    dpre = torch.empty(c, world * R, 2 * F, dtype=dt, device=dev)
-    dxp = torch.empty(c, world * R, H, dtype=dt, device=dev)
+    g2 = buf.get_tensor((world * rl, g_local.shape[1]), g_local.dtype, "mpu_dy")
+    gw = [comm.all_gather_into(g2[world * o:world * (o + r)], g_local[o:o + r], group=group,
+                               async_op=True) for o, r in pieces]
+    xt = buf.get_tensor((world * rl, H), dt, "mpu")
+    xw = [comm.all_gather_into(xt[world * o:world * (o + r)], x_local[o:o + r], group=group,
+                               async_op=True) for o, r in pieces]
+    dpre = torch.empty(world * rl, 2 * F, dtype=dt, device=dev)
+    dxp = torch.empty(world * rl, H, dtype=dt, device=dev)
     dx = torch.empty(rl, H, dtype=dt, device=dev)
     w2t, w1t = _weight_t_always(w2), _weight_t_always(w1)
     rs = []
-    for j in range(c):
+    for j, (o, r) in enumerate(pieces):
+        rows = slice(world * o, world * (o + r))
         gw[j].wait()
-        gemm_dglu(g2[j], w2t, pre3[j], kind, dpre[j])
-        gemm(dpre[j], w1t, dxp[j])
-        rs.append(comm.reduce_scatter_into(dx[j * R:(j + 1) * R], dxp[j], group=group,
-                                           async_op=True))
-    gw2 = _wgrad(w2, g2.view(c * world * R, -1), y, gaf)
+        gemm_dglu(g2[rows], w2t, pre[rows], kind, dpre[rows])
+        gemm(dpre[rows], w1t, dxp[rows])
+        rs.append(comm.reduce_scatter_into(dx[o:o + r], dxp[rows], group=group, async_op=True))
+    gw2 = _wgrad(w2, g2, y, gaf)
     for w in xw:
         w.wait()
-    gw1 = _wgrad(w1, dpre.view(c * world * R, 2 * F), xt.view(c * world * R, H), gaf)
+    gw1 = _wgrad(w1, dpre, xt, gaf)
     for w in rs:
         w.wait()
     return dx, gw1, gw2

@@ -69,6 +69,18 @@ def main():
                   lambda x=x, w1=w1, pre=pre, y=y: C.gemm_nt_glu(x, w1, 0, pre, y, []),
                   lambda g=g, w1=w1, prep=prep, yp=yp: [C.gemm_nt_glu(g[j], w1, 0, prep[j], yp[j], [])
                                                         for j in range(c)]))
+    # the MLP pipeline's own piece sizes (layers._sp_mlp_pieces: uneven where
+    # even pieces quantize the fc1 + GLU tiles), piece-major, no row remap
+    from epfl_megatron_amd.parallel.tensor.layers import _sp_mlp_pieces
+    sizes = _sp_mlp_pieces(M // tp, tp, 2 * F)
+    offs = [sum(sizes[:j]) for j in range(len(sizes))]
+    gu = [x[tp * o:tp * (o + n)] for o, n in zip(offs, sizes)]
+    preu = [prep.view(-1, 2 * F)[tp * o:tp * (o + n)] for o, n in zip(offs, sizes)]
+    yu = [yp.view(-1, F)[tp * o:tp * (o + n)] for o, n in zip(offs, sizes)]
+    cases.append((f"fc1+glu planned pieces {sizes}", 2.0 * M * 2 * F * H,
+                  lambda x=x, w1=w1, pre=pre, y=y: C.gemm_nt_glu(x, w1, 0, pre, y, []),
+                  lambda gu=gu, w1=w1, preu=preu, yu=yu: [C.gemm_nt_glu(a, w1, 0, b_, c_, [])
+                                                          for a, b_, c_ in zip(gu, preu, yu)]))
     w2 = r(H, F)
     yfull = r(M, F)
     o2 = torch.empty(M, H, device=dev, dtype=dt)
@@ -77,6 +89,18 @@ def main():
                   lambda y=yfull, w2=w2, o2=o2: C.gemm_nt(y, w2, o2),
                   lambda y=yfull, w2=w2, partp=partp: [C.gemm_nt(y[j * tp * R:(j + 1) * tp * R], w2,
                                                                  partp[j]) for j in range(c)]))
+    # the whole MLP forward (fc1 + GLU, fc2) as the pipeline runs it: even
+    # pieces vs the planned ones
+    o2b = torch.empty(M, H, device=dev, dtype=dt)
+
+    def mlp(parts, x=x, w1=w1, w2=w2, pre=pre, y=y, o2b=o2b):
+        for o, n in parts:
+            rows = slice(tp * o, tp * (o + n))
+            C.gemm_nt_glu(x[rows], w1, 0, pre[rows], y[rows], [])
+            C.gemm_nt(y[rows], w2, o2b[rows])
+    even = [(j * R, R) for j in range(c)]
+    cases.append((f"mlp fwd planned {sizes} vs even", 2.0 * M * 3 * F * H,
+                  lambda: mlp(even), lambda: mlp(list(zip(offs, sizes)))))
     # reduce-scatter side (attention out, fc2): the pieces read through a_map
     for name, k in (("o_proj", H // tp), ("fc2", F)):
         x, w = r(M, k), r(H, k)

@@ -384,3 +384,18 @@ def test_llama_context_parallel_document_masks():
     for cp in (2, 4):
         got = _losses(run_dist(_train, cp, argv + ["--context_parallel_size", str(cp)], 3))
         _check(base, got)
+
+
+@pytest.mark.parametrize("tp,pieces", [(2, "5,11"), (8, "1,3")])
+def test_llama_sp_mlp_uneven_pieces(llama_ref, monkeypatch, tp, pieces):
+    """The SP MLP pipeline with uneven pieces (layers._sp_mlp_pieces picks them
+    where even pieces quantize the fc1 + GLU GEMM): forced here, it trains like
+    TP = 1, with every collective's shapes checked (EMA_COMM_CHECK)."""
+    monkeypatch.setenv("EMA_SP_MLP_PIECES", pieces)
+    monkeypatch.setenv("EMA_COMM_CHECK", "1")
+    argv = TINY_LLAMA if tp == 2 else TINY_LLAMA8
+    base = llama_ref if tp == 2 else _losses(run_dist(_train, 1, TINY_LLAMA8 + _mb(2, 4), 3))
+    mb = ["--micro_batch_size", "2", "--global_batch_size", "4"] if tp == 2 else _mb(2, 4)
+    got = _losses(run_dist(_train, tp, argv + mb + ["--tensor_model_parallel_size", str(tp),
+                                                    "--sequence_parallel"], 3))
+    _check(base, got, tol=5e-5)
