@@ -641,43 +641,22 @@ class _GluMLPFn(torch.autograd.Function):
 # on RCCL's stream while piece j computes.  Reference (blocking forms):
 # megatron/core/tensor_parallel/layers.py:225-243, mappings.py:107-124, 244-246.
 def _sp_mlp_pieces(rl, world, n_fc1):
-    """Per-rank row counts of the SP MLP pipeline's pieces.
-
-    Even pieces (``EMA_SP_CHUNKS``) unless they quantize the fc1 + GLU GEMM
-    (256 x 256 tiles over the CUs) into more rounds than the monolithic
-    product: Llama-2-7B at TP 8 (16384 rows, 2F = 2752: 11 tile columns) in
-    two 32-tile-row pieces runs 2 + 2 rounds against 3 (pieces / mono 1.255,
-    profiles/r4d_sp_pieces.txt).  Then the first piece takes the largest
-    tile-aligned row count whose tiles fill whole rounds and the second the
-    rest (23 + 41 tile rows: 1 + 2 rounds).  ``EMA_SP_MLP_PIECES=r0,r1,...``
-    forces the split (tests)."""
+    """Per-rank row counts of the SP MLP pipeline's pieces: ``EMA_SP_CHUNKS``
+    even pieces.  The pipeline takes any split (``EMA_SP_MLP_PIECES=r0,r1,...``
+    forces one; the equivalence tests run uneven pieces).  An uneven split
+    sized to the fc1 + GLU tile rounds (Llama-2-7B TP8: 736 + 1312 rows per
+    rank, 1 + 2 rounds instead of 2 + 2) cut that product's piece cost from
+    1.239x to 1.033x of the monolithic GEMM and the MLP forward by 8.5 %, but
+    the uneven fc1 dgrad / fc2 pieces lost more: the TP8 proxy step ran 4 %
+    slower (profiles/r4ab_sp_pieces.txt, profiles/r4ac_sp_pieces_proxy_ab.txt),
+    so the split stays even."""
     forced = os.environ.get("EMA_SP_MLP_PIECES")
     if forced:
         sizes = [int(v) for v in forced.split(",")]
         if sum(sizes) == rl and all(v > 0 for v in sizes):
             return sizes
     c = _sp_pieces(rl)
-    even = [rl // c] * c
-    if c == 1 or not torch.cuda.is_available() or (world * rl) % 256:
-        return even
-    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    ntile = -(-n_fc1 // 256)
-    mt = world * rl // 256
-
-    def rounds(m):
-        return -(-m * ntile // cus)
-    mono = rounds(mt)
-    if sum(rounds(world * r // 256) for r in even) <= mono or (world * (rl // c)) % 256:
-        return even
-    per_round = cus // ntile
-    for k in range(1, mono):
-        m1 = k * per_round
-        if m1 >= mt:
-            break
-        if rounds(m1) + rounds(mt - m1) <= mono and (m1 * 256) % world == 0:
-            r1 = m1 * 256 // world
-            return [r1, rl - r1]
-    return even
+    return [rl // c] * c
 
 
 def _sp_mlp_forward(x_local, w1, w2, kind):

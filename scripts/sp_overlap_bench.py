@@ -71,8 +71,10 @@ def main():
                                                         for j in range(c)]))
     # the MLP pipeline's own piece sizes (layers._sp_mlp_pieces: uneven where
     # even pieces quantize the fc1 + GLU tiles), piece-major, no row remap
-    from epfl_megatron_amd.parallel.tensor.layers import _sp_mlp_pieces
-    sizes = _sp_mlp_pieces(M // tp, tp, 2 * F)
+    # (the tile-round plan of round 4: 23 + 41 tile rows of 256; the pipeline
+    # keeps even pieces, see layers._sp_mlp_pieces)
+    m1 = 256 // -(-2 * F // 256) * 256 // tp
+    sizes = [m1, M // tp - m1]
     offs = [sum(sizes[:j]) for j in range(len(sizes))]
     gu = [x[tp * o:tp * (o + n)] for o, n in zip(offs, sizes)]
     preu = [prep.view(-1, 2 * F)[tp * o:tp * (o + n)] for o, n in zip(offs, sizes)]
