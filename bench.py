@@ -479,7 +479,7 @@ def main(argv=None):
             "config": {"model": label, "global_batch": par["gbs"], "seq_len": par["seq"],
                        "micro_batch": par["mbs"], "num_micro_batches": par["nmicro"],
                        "parallelism": parallel},
-            "tokens_per_sec_per_gpu": round(per_gpu, 1),
+            "tokens_per_sec_per_gpu": round(per_gpu, 2),
             "mfu": round(mfu, 4),
             "tflops_per_gpu": round(per_gpu * fpt / 1e12, 1),
             "flops_per_token": fpt,
