@@ -1142,6 +1142,35 @@ void transpose16(const at::Tensor& src, at::Tensor dst) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- xGMI one-shot all-reduce
+// (csrc/xgmi_allreduce.hip; parallel/xgmi.py exchanges the handles)
+std::tuple<int64_t, at::Tensor> xgmi_create(int64_t rank, int64_t world, int64_t cap) {
+  at::Tensor h = at::empty({ema::xgmi_handle_size()}, at::TensorOptions().dtype(at::kByte));
+  const int64_t id = ema::xgmi_create((int)rank, (int)world, cap, h.data_ptr());
+  return {id, h};
+}
+void xgmi_open(int64_t id, const at::Tensor& handles) {
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
+                  handles.dim() == 2 && handles.size(1) == ema::xgmi_handle_size(),
+              "xgmi_open: handles uint8 [world, handle_size] on the CPU");
+  ema::xgmi_open(id, handles.data_ptr());
+}
+void xgmi_all_reduce(int64_t id, const at::Tensor& inp, at::Tensor out) {
+  check_gpu(inp, "inp");
+  check_gpu(out, "out");
+  const int dt = dtype_code(inp);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16 || dt == ema::DT_F32, "xgmi_all_reduce: dtype");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() &&
+                  inp.is_contiguous() && out.is_contiguous(),
+              "xgmi_all_reduce: contiguous in / out of one dtype and size");
+  const int64_t nbytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(nbytes % 16 == 0 && reinterpret_cast<uintptr_t>(inp.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "xgmi_all_reduce: 16-byte aligned, 16-byte sized buffers");
+  TORCH_CHECK(nbytes <= ema::xgmi_capacity(id), "xgmi_all_reduce: message exceeds the registered capacity");
+  ema::xgmi_all_reduce(id, inp.data_ptr(), out.data_ptr(), nbytes, dt, cur_stream());
+}
+
 void register_gemm_lt(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1213,6 +1242,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("docs"), py::arg("coff") = -1);
   m.def("fa_set_stamps", &fa_set_stamps);
   m.def("greedy_tail", &greedy_tail);
+  m.def("xgmi_create", &xgmi_create);
+  m.def("xgmi_open", &xgmi_open);
+  m.def("xgmi_all_reduce", &xgmi_all_reduce);
+  m.def("xgmi_error", [](int64_t id) { return ema::xgmi_error(id); });
+  m.def("xgmi_destroy", [](int64_t id) { ema::xgmi_destroy(id); });
   m.def("flash_decode", &flash_decode, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"),
         py::arg("b"), py::arg("sk"), py::arg("nq"), py::arg("nkv"), py::arg("hd"), py::arg("qs"),
         py::arg("ks"), py::arg("vs"), py::arg("os"), py::arg("scale"), py::arg("kv_len"),

@@ -211,6 +211,20 @@ int flash_decode_counters(int b, int nq, int nkv);
 void flash_decode(const DecodeParams& p, int dt, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, int dt, hipStream_t s);
 
+// ---- xgmi_allreduce.hip --------------------------------------------------------------------------
+// One-shot all-reduce over IPC-mapped peer memory (small messages; see the file
+// header).  create: allocate this rank's region and write its IPC handle
+// (xgmi_handle_size() bytes) to handle_out; open: map the peers' handles
+// ([world][handle] bytes); all_reduce: out = sum over ranks of in (in-place ok,
+// nbytes a multiple of 16, <= cap), on stream s.
+int64_t xgmi_create(int rank, int world, int64_t cap, void* handle_out);
+int xgmi_handle_size();
+void xgmi_open(int64_t id, const void* handles);
+int64_t xgmi_capacity(int64_t id);
+void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s);
+int xgmi_error(int64_t id);
+void xgmi_destroy(int64_t id);
+
 // ---- gemm_wgrad.hip ------------------------------------------------------------------------------
 // G[N,K] (+)= dY[M,N]^T X[M,K]; dY/X bf16|fp16 row-major, G fp32 row-major.
 // Split-K plan of a shape: tiles [0, main_tiles) run unsplit, tiles

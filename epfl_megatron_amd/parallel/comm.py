@@ -42,6 +42,7 @@ _GROUP_SIZES = {}  # name -> ranks in the group (bus-bandwidth factors of the re
 _PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
 _LOOPBACK = {}  # id(group) -> simulated size (--simulated_tensor_parallel_size)
 _LOOPBACK_FILLED = set()  # (data_ptr, numel) of all-gather outputs zero-filled once
+_XGMI = {}  # id(group) -> parallel.xgmi.XgmiAllReduce (one-shot small all-reduce)
 
 
 class CommRaceError(RuntimeError):
@@ -74,6 +75,24 @@ def set_loopback(group, world):
     name = _GROUP_NAMES.get(id(group))
     if name is not None and world:
         _GROUP_SIZES[name] = int(world)
+
+
+def enable_xgmi_allreduce(group, cap_bytes):
+    """Route small sum all-reduces on ``group`` (contiguous bf16 / fp16 / fp32
+    CUDA tensors of at most ``cap_bytes``) through the one-shot xGMI kernel
+    (``parallel/xgmi.py``); RCCL keeps everything else.  Collective over the
+    group (handle exchange).  ``cap_bytes`` 0 / None disables."""
+    old = _XGMI.pop(id(group), None)
+    if old is not None:
+        old.close()
+    if cap_bytes:
+        from .xgmi import XgmiAllReduce  # noqa: PLC0415
+        _XGMI[id(group)] = XgmiAllReduce(group, cap_bytes)
+    return _XGMI.get(id(group))
+
+
+def xgmi_allreduce_of(group):
+    return _XGMI.get(id(group))
 
 
 def loopback_size(group):
@@ -239,6 +258,12 @@ def all_reduce(tensor, group=None, async_op=False, op="sum"):
     rop = _op(op)
     if id(group) in _LOOPBACK:
         return _issue("all_reduce", group, tensor, tensor, lambda a: None, async_op)
+    xg = _XGMI.get(id(group))
+    if xg is not None and rop == dist.ReduceOp.SUM and xg.eligible(tensor):
+        # stream-ordered kernel: complete for the current stream when issued
+        def oneshot(a):
+            xg(tensor)
+        return _issue("all_reduce_xgmi", group, tensor, tensor, oneshot, async_op)
     return _issue("all_reduce", group, tensor, tensor,
                   lambda a: dist.all_reduce(tensor, op=rop, group=group, async_op=a), async_op)
 

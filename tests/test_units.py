@@ -464,3 +464,59 @@ def test_decode_pack_layout():
         assert v[bt, h, wv, s, q, pr, e] == w[f if pr < 4 else F + f, wv * 32 * S + 32 * s + 8 * q + e]
     assert not dp.packable(torch.zeros(16, 384).bfloat16())
     assert not dp.packable(torch.zeros(16, 512))
+
+
+# ------------------------------------------------- one-shot all-reduce routing
+class _FakeOneShot:
+    """Stands in for parallel.xgmi.XgmiAllReduce on the CPU: eligible for
+    small tensors, performs the reduction through the process group."""
+
+    def __init__(self, group, cap):
+        self.group, self.cap, self.calls = group, cap, 0
+
+    def eligible(self, t):
+        return t.is_contiguous() and t.numel() * t.element_size() <= self.cap
+
+    def __call__(self, t):
+        self.calls += 1
+        dist.all_reduce(t, group=self.group)
+        return t
+
+
+def _oneshot_routing(rank, world):
+    from epfl_megatron_amd.parallel import comm
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(list(range(world)))
+    fake = _FakeOneShot(grp, 64)
+    comm._XGMI[id(grp)] = fake
+    comm.report(reset=True)
+    small = torch.full((16,), float(rank + 1))          # 64 B: one-shot path
+    big = torch.full((64,), float(rank + 1))            # 256 B: process group
+    mx = torch.full((4,), float(rank))                  # max: never one-shot
+    comm.all_reduce(small, group=grp)
+    comm.all_reduce(big, group=grp)
+    comm.all_reduce(mx, group=grp, op="max")
+    w = comm.all_reduce(small, group=grp, async_op=True)
+    w.wait()
+    rep = comm.report()
+    comm._XGMI.pop(id(grp))
+    return fake.calls, sorted(k.split("/")[0] for k in rep), small[0].item(), big[0].item(), mx[0].item()
+
+
+def test_xgmi_oneshot_routing_cpu():
+    """comm.all_reduce sends eligible sum all-reduces of a registered group to
+    the one-shot communicator (accounted as all_reduce_xgmi) and everything
+    else to the process group."""
+    for calls, keys, s, b, m in run_dist(_oneshot_routing, 2):
+        assert calls == 2
+        assert keys == ["all_reduce", "all_reduce_xgmi"]
+        assert s == 6.0 and b == 3.0 and m == 1.0
+
+
+def test_xgmi_flag_validation():
+    from epfl_megatron_amd.config.arguments import parse_args, validate_args
+    base = ["--num_layers", "2", "--hidden_size", "64", "--num_attention_heads", "4",
+            "--seq_length", "16", "--max_position_embeddings", "16", "--micro_batch_size", "1"]
+    args = parse_args(args_list=base + ["--tp_xgmi_allreduce_kb", "6"])
+    with pytest.raises(Exception, match="tp_xgmi_allreduce_kb"):
+        validate_args(args)

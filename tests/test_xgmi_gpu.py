@@ -1,0 +1,102 @@
+"""One-shot xGMI all-reduce (csrc/xgmi_allreduce.hip, parallel/xgmi.py).
+
+Several processes share the one GPU of the test box: each maps the others'
+regions through same-device IPC handles, so the flag / parity protocol and the
+kernel are the ones a multi-GPU TP group runs (the transport there is xGMI).
+Oracle: the fp32 sum of every rank's input in rank order, rounded once to the
+dtype (the kernel's exact arithmetic), and bitwise equality across ranks.
+"""
+import pytest
+import torch
+
+from dist_utils import run_dist
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+
+def _inputs(world, n, dt, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(n, generator=g).to(dt) for _ in range(world)]
+
+
+def _oracle(xs):
+    acc = torch.zeros(xs[0].shape, dtype=torch.float32)
+    for x in xs:
+        acc += x.float()
+    return acc.to(xs[0].dtype)
+
+
+def _rank(rank, world):
+    import torch.distributed as dist
+
+    from epfl_megatron_amd.parallel import comm
+    from epfl_megatron_amd.parallel.xgmi import XgmiAllReduce
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    xg = XgmiAllReduce(None, cap_bytes=256 * 1024)
+    bad = []
+    # sizes: one partial chunk, a chunk boundary + tail, many chunks; 30 rounds
+    # cycle the epochs through both parities many times
+    for it in range(30):
+        for dt in DTYPES:
+            for n in (8, 2048 + 8, 40000):
+                xs = _inputs(world, n, dt, 1000 * it + n)
+                t = xs[rank].cuda()
+                if it % 2:
+                    xg(t)
+                    got = t
+                else:
+                    got = torch.empty_like(t)
+                    xg(t, got)
+                torch.cuda.synchronize()
+                if not torch.equal(got.cpu(), _oracle(xs)):
+                    bad.append((it, str(dt), n))
+    xg.check()
+    # captured in a hipGraph: replays advance the device-side epochs
+    t = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        xg(t)
+    for rep in range(5):
+        xs = _inputs(world, 4096, torch.bfloat16, 77 + rep)
+        t.copy_(xs[rank])
+        g.replay()
+        torch.cuda.synchronize()
+        if not torch.equal(t.cpu(), _oracle(xs)):
+            bad.append(("graph", rep))
+    xg.check()
+    # routing through comm.all_reduce: small sum -> one-shot kernel, the rest
+    # (too large for the registered capacity) -> the process group
+    grp = dist.group.WORLD
+    comm._XGMI[id(grp)] = xg
+    comm.report(reset=True)
+    xs = _inputs(world, 1024, torch.float32, 5)
+    t = xs[rank].cuda()
+    comm.all_reduce(t, group=grp)
+    big = torch.ones(128 * 1024, dtype=torch.float32, device="cuda")
+    comm.all_reduce(big, group=grp)
+    torch.cuda.synchronize()
+    rep = comm.report()
+    routed = [k for k in rep if k.startswith("all_reduce_xgmi")]
+    if not torch.equal(t.cpu(), _oracle(xs)) or not routed or not torch.all(big == world):
+        bad.append(("comm", sorted(rep)))
+    comm._XGMI.pop(id(grp))
+    xg.check()
+    out = (bad, t.cpu())
+    dist.barrier()
+    xg.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_oneshot_allreduce(world):
+    res = run_dist(_rank, world, timeout=300)
+    for bad, _ in res:
+        assert not bad, bad
+    # every rank holds the same bits
+    for _, t in res[1:]:
+        assert torch.equal(t, res[0][1])
