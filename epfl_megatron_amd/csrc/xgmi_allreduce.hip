@@ -87,8 +87,8 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   if (valid) {
     constexpr int N = V16<T>::N;
     float acc[N];

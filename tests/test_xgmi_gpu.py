@@ -69,6 +69,28 @@ def _rank(rank, world):
         if not torch.equal(t.cpu(), _oracle(xs)):
             bad.append(("graph", rep))
     xg.check()
+    # latency of an 8 KiB call (ranks sharing the GPU: an upper bound on the
+    # kernel's own cost, with no xGMI hop in it): eager and graph-replayed
+    import time
+    for _ in range(20):
+        xg(t)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        xg(t)
+    torch.cuda.synchronize()
+    eager_us = (time.perf_counter() - t0) / 200 * 1e6
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        g.replay()
+    torch.cuda.synchronize()
+    graph_us = (time.perf_counter() - t0) / 200 * 1e6
+    xg.check()
+    if rank == 0:
+        print(f"xgmi one-shot 8 KiB bf16, world {world} on one GPU: eager {eager_us:.1f} us/call, "
+              f"graph replay {graph_us:.1f} us/call", flush=True)
     # routing through comm.all_reduce: small sum -> one-shot kernel, the rest
     # (too large for the registered capacity) -> the process group
     grp = dist.group.WORLD
