@@ -1,7 +1,7 @@
 // Weight-streaming GEMM for decode-sized batches on gfx950, with the decode
 // step's elementwise work fused into its prologue / epilogue:
 //
-//     Y[M, N] = f(norm(X)[M, K] · W[N, K]^T)        M <= 16, bf16/fp16, fp32 accumulate
+//     Y[M, N] = f(norm(X)[M, K] · W[N, K]^T)        M <= 32, bf16/fp16, fp32 accumulate
 //
 // A token-by-token decode step multiplies a handful of rows by every weight
 // of the model: the time is the weight stream from HBM.  hipBLASLt's skinny
@@ -32,7 +32,8 @@
 //     (pairs 2i, 2i+1: inside one lane's 4 features), q goes to Y [M, nq*hd],
 //     k and v straight into the KV cache slot (device-resident slot index, so
 //     the step is graph-capturable).
-// Shapes: M <= 16, N % 16 == 0, K % 128 == 0 (checked by the host).
+// Shapes: M <= 32 (17-32 rows: two row blocks per W fragment in the
+// per-block kernel), N % 16 == 0, K % 128 == 0 (checked by the host).
 //
 // Packed weights (p.packed, 8-wave forms, K % 256 == 0).  In row-major W a
 // wave's A-operand load (lane L: row L & 15, 8 k at 8 (L >> 4)) touches 16
@@ -82,21 +83,26 @@ template <typename T, int EPI>
 struct EpiPre {
   typename fa::MT<T>::x4 rv{};
   float c[2] = {0.f, 0.f}, s[2] = {0.f, 0.f};
-  int64_t pos = 0, slot = 0;
+  int pos = 0;       // (32-bit: two row blocks' 64-bit positions and slots spilled)
+  int64_t slot = 0;  // uniform: scalar registers
 };
 
 template <typename T, int EPI>
-__device__ __forceinline__ void epi_init(const SkinnyArgs& p, int lane, EpiPre<T, EPI>& e) {
+__device__ __forceinline__ void epi_init(const SkinnyArgs& p, int lane, EpiPre<T, EPI>& e,
+                                         int moff = 0) {
   if constexpr (EPI == EPI_QKV) {
-    const int m = lane & 15;
-    e.pos = m < p.M ? p.pos[(int64_t)m * p.pos_sb] : 0;
-    e.slot = p.slot_ptr ? *p.slot_ptr : p.slot;
+    const int m = (lane & 15) + moff;
+    e.pos = m < p.M ? (int)p.pos[(int64_t)m * p.pos_sb] : 0;
+    const int64_t sl = p.slot_ptr ? *p.slot_ptr : p.slot;
+    e.slot = (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(sl & 0xffffffffll)) |
+             ((int64_t)__builtin_amdgcn_readfirstlane((int)(sl >> 32)) << 32);
   }
 }
 
 template <typename T, int EPI>
-__device__ __forceinline__ void epi_prefetch(const SkinnyArgs& p, int blk, int lane, EpiPre<T, EPI>& e) {
-  const int m = lane & 15, n = blk * 16 + 4 * (lane >> 4);
+__device__ __forceinline__ void epi_prefetch(const SkinnyArgs& p, int blk, int lane, EpiPre<T, EPI>& e,
+                                             int moff = 0) {
+  const int m = (lane & 15) + moff, n = blk * 16 + 4 * (lane >> 4);
   if (m >= p.M) return;
   if constexpr (EPI == EPI_RES) {
     e.rv = *reinterpret_cast<const typename fa::MT<T>::x4*>((const T*)p.res + (int64_t)m * p.ldr + n);
@@ -104,8 +110,8 @@ __device__ __forceinline__ void epi_prefetch(const SkinnyArgs& p, int blk, int l
   if constexpr (EPI == EPI_QKV) {
     const int hd = p.hd, per_g = (p.r + 2) * hd;
     const int d = (n - (n / per_g) * per_g) % hd;
-    const float* cr = p.cos + e.pos * (hd / 2) + d / 2;
-    const float* sr = p.sin + e.pos * (hd / 2) + d / 2;
+    const float* cr = p.cos + (int64_t)e.pos * (hd / 2) + d / 2;
+    const float* sr = p.sin + (int64_t)e.pos * (hd / 2) + d / 2;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       e.c[j] = cr[j];
@@ -116,10 +122,12 @@ __device__ __forceinline__ void epi_prefetch(const SkinnyArgs& p, int blk, int l
 
 template <typename T, int EPI, int ACT>
 __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4& t, int lane,
-                                         int half = -1, const EpiPre<T, EPI>* pre = nullptr) {
+                                         int half, const EpiPre<T, EPI>& pre, bool use_pre,
+                                         int moff = 0) {
   const int M = p.M;
-  // D layout: lane holds column m = lane & 15, rows (features) 4 (lane >> 4) + i
-  const int m = lane & 15, nr = 4 * (lane >> 4);
+  // D layout: lane holds column m = lane & 15 (+ moff: the row block), rows
+  // (features) 4 (lane >> 4) + i
+  const int m = (lane & 15) + moff, nr = 4 * (lane >> 4);
   typename fa::MT<T>::x4 o;
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = (T)t[i];
@@ -143,7 +151,7 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
   if (m >= M) return;
   const int n = blk * 16 + nr;
   if constexpr (EPI == EPI_RES) {
-    const typename fa::MT<T>::x4 rv = pre ? pre->rv :
+    const typename fa::MT<T>::x4 rv = use_pre ? pre.rv :
         *reinterpret_cast<const typename fa::MT<T>::x4*>((const T*)p.res + (int64_t)m * p.ldr + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = (T)((float)o[i] + (float)rv[i]);
@@ -152,13 +160,13 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
     const int hd = p.hd, per_g = (p.r + 2) * hd;
     const int g = n / per_g, rem = n - g * per_g, h = rem / hd, d = rem - h * hd;
     if (h <= p.r) {  // q heads and the k head: rotate pairs (d, d+1), (d+2, d+3)
-      const int64_t pos = pre ? 0 : p.pos[(int64_t)m * p.pos_sb];
+      const int64_t pos = use_pre ? 0 : p.pos[(int64_t)m * p.pos_sb];
       const float* cr = p.cos + pos * (hd / 2) + d / 2;
       const float* sr = p.sin + pos * (hd / 2) + d / 2;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float x0 = (float)o[2 * j], x1 = (float)o[2 * j + 1];
-        const float c = pre ? pre->c[j] : cr[j], sn = pre ? pre->s[j] : sr[j];
+        const float c = use_pre ? pre.c[j] : cr[j], sn = use_pre ? pre.s[j] : sr[j];
         o[2 * j] = (T)(x0 * c - x1 * sn);
         o[2 * j + 1] = (T)(x0 * sn + x1 * c);
       }
@@ -167,7 +175,7 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
     if (h < p.r) {
       dst = y + (int64_t)m * p.ldy + (int64_t)(g * p.r + h) * hd + d;
     } else {
-      const int64_t slot = pre ? pre->slot : p.slot_ptr ? *p.slot_ptr : p.slot;
+      const int64_t slot = use_pre ? pre.slot : p.slot_ptr ? *p.slot_ptr : p.slot;
       T* cache = (T*)(h == p.r ? p.kcache : p.vcache);
       dst = cache + slot * p.c_ss + (int64_t)m * p.c_sb + (int64_t)g * hd + d;
     }
@@ -181,12 +189,14 @@ __device__ __forceinline__ void epilogue(const SkinnyArgs& p, int blk, const f4&
 #define SKINNY_U 8  // k-steps of W / X (/ gamma) loads in flight per wave
 #endif
 
-template <typename T, int WAVES, bool NORM, int EPI, int ACT, bool PACKED>
+// MB: 16-row blocks of X (1: M <= 16; 2: M <= 32 -- every W fragment feeds
+// one MFMA per row block, so the weight stream is read once for 32 rows).
+template <typename T, int WAVES, bool NORM, int EPI, int ACT, bool PACKED, int MB>
 __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
   constexpr int U = SKINNY_U;
-  __shared__ f4 part[WAVES][64];
-  __shared__ float ssq[WAVES][16];
+  __shared__ f4 part[WAVES][MB][64];
+  __shared__ float ssq[WAVES][16 * MB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = p.M, N = p.N, K = p.K;
   const T* __restrict__ x = (const T*)p.x;
@@ -200,85 +210,103 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
   static_assert(!PACKED || WAVES == 8, "the packed layout is cut for 8 waves");
   const T* wr = PACKED ? w + ((int64_t)blockIdx.x * WAVES + wave) * steps * 512 + 8 * lane
                        : w + w_row<EPI>(blockIdx.x, r, N) * K + kbeg + kc;
-  const bool xon = r < M;
-  const T* xr = x + (int64_t)(xon ? r : 0) * K + kbeg + kc;
+  bool xon[MB];
+  const T* xr[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    xon[mb] = r + 16 * mb < M;
+    xr[mb] = x + (int64_t)(xon[mb] ? r + 16 * mb : 0) * K + kbeg + kc;
+  }
   const T* gr = NORM ? (const T*)p.norm_w + kbeg + kc : nullptr;
   const int nblk = steps / U;  // full ring blocks; the < U leftover steps run after them
 
   // Ring of U k-steps: the W fragment (nontemporal: each weight byte is read
-  // once per step), the X fragment and (NORM) the gamma fragment, refilled
+  // once per step), the X fragments and (NORM) the gamma fragment, refilled
   // U steps ahead right after each MFMA consumes its slot, so U k-steps of
   // loads stay in flight through the whole stream.  Issued BEFORE the RMSNorm
   // prologue: the weight stream starts at kernel entry, not after the norm's
   // reduction and barrier.
-  x8 a[U], xv[U], gv[U];
+  x8 a[U], xv[MB][U], gv[U];
   if (nblk > 0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * u));
-      xv[u] = *reinterpret_cast<const x8*>(xr + 32 * u);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) xv[mb][u] = *reinterpret_cast<const x8*>(xr[mb] + 32 * u);
       if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * u);
     }
   }
 
-  float rs = 1.f;  // rstd of X row r (NORM)
+  float rs[MB];  // rstd of X rows r + 16 mb (NORM)
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) rs[mb] = 1.f;
   if constexpr (NORM) {
     // sum of squares of this wave's X slice: 8 loads issued per round before
     // any is used (a load-then-use loop waits out one L2 round trip per step)
-    float ss = 0.f;
-    for (int s0 = 0; s0 < steps; s0 += 8) {
-      x8 v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int s = s0 + i < steps ? s0 + i : steps - 1;
-        v[i] = *reinterpret_cast<const x8*>(xr + 32 * s);
-      }
+    for (int mb = 0; mb < MB; ++mb) {
+      float ss = 0.f;
+      for (int s0 = 0; s0 < steps; s0 += 8) {
+        x8 v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float keep = s0 + i < steps ? 1.f : 0.f;
+        for (int i = 0; i < 8; ++i) {
+          const int s = s0 + i < steps ? s0 + i : steps - 1;
+          v[i] = *reinterpret_cast<const x8*>(xr[mb] + 32 * s);
+        }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = (float)v[i][e];
-          ss += keep * f * f;
+        for (int i = 0; i < 8; ++i) {
+          const float keep = s0 + i < steps ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)v[i][e];
+            ss += keep * f * f;
+          }
         }
       }
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (lane < 16) ssq[wave][16 * mb + lane] = ss;
     }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 16) ssq[wave][lane] = ss;
     __syncthreads();
-    float tot = 0.f;
 #pragma unroll
-    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
-    rs = rsqrtf(tot / (float)K + p.eps);
+    for (int mb = 0; mb < MB; ++mb) {
+      float tot = 0.f;
+#pragma unroll
+      for (int i = 0; i < WAVES; ++i) tot += ssq[i][16 * mb + r];  // fixed order
+      rs[mb] = rsqrtf(tot / (float)K + p.eps);
+    }
   }
-  // B operand: X (or its RMSNorm, rounded like rmsnorm_fwd_k)
-  auto bop = [&](const x8& v, const x8& g) {
+  // B operand: X (or its RMSNorm, rounded like rmsnorm_fwd_k) of row block mb
+  auto bop = [&](const x8& v, const x8& g, int mb) {
     x8 o;
     if constexpr (!NORM) {
       o = v;
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const T xn = (T)((float)v[e] * rs);
+        const T xn = (T)((float)v[e] * rs[mb]);
         o[e] = (T)((float)xn * (float)g[e]);
       }
     }
-    if (!xon) o = x8{};
+    if (!xon[mb]) o = x8{};
     return o;
   };
 
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = f4{0.f, 0.f, 0.f, 0.f};
   // one ring block; REFILL: reload each slot U steps ahead once consumed
   auto block = [&](int blk, auto refill_c) {
     constexpr bool REFILL = decltype(refill_c)::value;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc = mfma16x16x32<T>(a[u], bop(xv[u], gv[u]), acc);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma16x16x32<T>(a[u], bop(xv[mb][u], gv[u], mb), acc[mb]);
       if constexpr (REFILL) {
         const int s = (blk + 1) * U + u;
         a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * s));
-        xv[u] = *reinterpret_cast<const x8*>(xr + 32 * s);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) xv[mb][u] = *reinterpret_cast<const x8*>(xr[mb] + 32 * s);
         if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * s);
       }
       // keep {MFMA u, refill u} in program order: hipcc would otherwise
@@ -296,21 +324,29 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
     for (int u = 0; u < U - 1; ++u) {
       if (u < left) {
         a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + WS * (s0 + u)));
-        xv[u] = *reinterpret_cast<const x8*>(xr + 32 * (s0 + u));
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) xv[mb][u] = *reinterpret_cast<const x8*>(xr[mb] + 32 * (s0 + u));
         if constexpr (NORM) gv[u] = *reinterpret_cast<const x8*>(gr + 32 * (s0 + u));
       }
     }
 #pragma unroll
     for (int u = 0; u < U - 1; ++u)
-      if (u < left) acc = mfma16x16x32<T>(a[u], bop(xv[u], gv[u]), acc);
+      if (u < left) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma16x16x32<T>(a[u], bop(xv[mb][u], gv[u], mb), acc[mb]);
+      }
   }
-  part[wave][lane] = acc;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) part[wave][mb][lane] = acc[mb];
   __syncthreads();
   if (wave != 0) return;
-  f4 t = part[0][lane];
 #pragma unroll
-  for (int i = 1; i < WAVES; ++i) t += part[i][lane];  // fixed order: deterministic
-  epilogue<T, EPI, ACT>(p, blockIdx.x, t, lane);
+  for (int mb = 0; mb < MB; ++mb) {
+    f4 t = part[0][mb][lane];
+#pragma unroll
+    for (int i = 1; i < WAVES; ++i) t += part[i][mb][lane];  // fixed order: deterministic
+    epilogue<T, EPI, ACT>(p, blockIdx.x, t, lane, -1, EpiPre<T, EPI>{}, false, 16 * mb);
+  }
 }
 
 // Persistent form for K = 8 waves x 32 x STEPS (STEPS 16 / 32: the 4096 / 8192
@@ -326,14 +362,15 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
 //     the next block's first U k-steps, so the stream never drains;
 //   * per block, the 8 partial tiles meet in a double-buffered LDS slot and
 //     wave 0 runs the epilogue while the other waves stream the next block.
-template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U, bool PACKED>
+template <typename T, bool NORM, int EPI, int ACT, int STEPS, int U, bool PACKED, int MB>
 __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   typedef typename fa::MT<T>::x8 x8;
   constexpr int WAVES = 8;
   static_assert(STEPS % U == 0, "ring must tile the k-steps");
   static_assert(!NORM || STEPS == 16, "the normed forms keep 64 gamma chunks per wave");
-  __shared__ f4 part[2][WAVES][64];
-  __shared__ float ssq[WAVES][16];
+  static_assert(MB == 1 || STEPS == 16, "two row blocks keep 2 x 16 X fragments in registers");
+  __shared__ f4 part[2][WAVES][MB][64];
+  __shared__ float ssq[WAVES][16 * MB];
   __shared__ x8 gsh[NORM ? WAVES : 1][64];  // NORM: each wave's gamma slice
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = p.M, N = p.N, K = p.K;
@@ -341,7 +378,9 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   const T* __restrict__ w = (const T*)p.w;
   const int kbeg = wave * STEPS * 32;
   const int r = lane & 15, kc = 8 * (lane >> 4);
-  const bool xon = r < M;
+  bool xon[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) xon[mb] = r + 16 * mb < M;
   const int nblocks = EPI == EPI_GLU ? N / 8 : N / 16;
   const int G = (int)gridDim.x, wg = blockIdx.x;
   // Work units of this workgroup: blocks wg, wg + G, ...  GLU tail: when the
@@ -375,10 +414,13 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
     return w + row * K + kbeg + kc;
   };
   int j = 0, blk = unit_blk(0), half = unit_half(0);
-  EpiPre<T, EPI> pre;  // wave 0: the epilogue operands of the current block
+  EpiPre<T, EPI> pre[MB];  // wave 0: the epilogue operands of the current block
   if (wave == 0) {
-    epi_init<T, EPI>(p, lane, pre);
-    epi_prefetch<T, EPI>(p, blk, lane, pre);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      epi_init<T, EPI>(p, lane, pre[mb], 16 * mb);
+      epi_prefetch<T, EPI>(p, blk, lane, pre[mb], 16 * mb);
+    }
   }
   const T* wr = wptr(0);
   const T* wn = wptr(nunits > 1 ? 1 : 0);
@@ -388,15 +430,16 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   // return in order, so X lands first and the norm prologue runs while the
   // ring's weight loads are in flight (issued the other way round, X came
   // back only after the whole ring and the first MFMA waited for the norm)
-  x8 xs[STEPS];
-  {
-    const T* xr = x + (int64_t)r * K + kbeg + kc;
-    if (xon) {
+  x8 xs[MB][STEPS];
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) xs[s] = *reinterpret_cast<const x8*>(xr + 32 * s);
+  for (int mb = 0; mb < MB; ++mb) {
+    const T* xr = x + (int64_t)(r + 16 * mb) * K + kbeg + kc;
+    if (xon[mb]) {
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) xs[mb][s] = *reinterpret_cast<const x8*>(xr + 32 * s);
     } else {
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) xs[s] = x8{};
+      for (int s = 0; s < STEPS; ++s) xs[mb][s] = x8{};
     }
   }
   // gamma: the wave's K slice is 64 chunks of 8, one 16-B load per lane,
@@ -406,48 +449,74 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   if constexpr (NORM) gl = *reinterpret_cast<const x8*>((const T*)p.norm_w + kbeg + 8 * lane);
   __builtin_amdgcn_sched_barrier(0);
   x8 a[U];
+  // Two normed row blocks keep 2 x 16 X fragments and spill ~0.5 KB per lane
+  // in this prologue whatever the order (ring after the norm spills least):
+  // the decode layer normalises 17-32 rows with the rmsnorm kernel and calls
+  // the un-normed forms instead (models/transformer.py _forward_decode_fused;
+  // profiles/r4ai_skinny_mb.txt, r4aj_skinny_mb.txt).
+  constexpr bool RING_FIRST = !(NORM && MB == 2);
+  if constexpr (RING_FIRST) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + ws * u));
+    for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + ws * u));
+  }
   if constexpr (NORM) {
-    float ss = 0.f;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s)
+    for (int mb = 0; mb < MB; ++mb) {
+      float ss = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)xs[s][e];
-        ss += f * f;
+      for (int s = 0; s < STEPS; ++s) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)xs[mb][s][e];
+          ss += f * f;
+        }
       }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 16) ssq[wave][lane] = ss;
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (lane < 16) ssq[wave][16 * mb + lane] = ss;
+    }
     gsh[wave][lane] = gl;
     __syncthreads();
-    float tot = 0.f;
 #pragma unroll
-    for (int i = 0; i < WAVES; ++i) tot += ssq[i][r];  // fixed order
-    const float rs = rsqrtf(tot / (float)K + p.eps);
-    // rounded like rmsnorm_fwd_k; step s, lane group q reads chunk 4 s + q
+    for (int mb = 0; mb < MB; ++mb) {
+      float tot = 0.f;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const x8 g = gsh[wave][4 * s + (lane >> 4)];
+      for (int i = 0; i < WAVES; ++i) tot += ssq[i][16 * mb + r];  // fixed order
+      const float rs = rsqrtf(tot / (float)K + p.eps);
+      // rounded like rmsnorm_fwd_k; step s, lane group q reads chunk 4 s + q
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const T xn = (T)((float)xs[s][e] * rs);
-        xs[s][e] = (T)((float)xn * (float)g[e]);
+      for (int s = 0; s < STEPS; ++s) {
+        const x8 g = gsh[wave][4 * s + (lane >> 4)];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const T xn = (T)((float)xs[mb][s][e] * rs);
+          xs[mb][s][e] = (T)((float)xn * (float)g[e]);
+        }
+        if (!xon[mb]) xs[mb][s] = x8{};
       }
-      if (!xon) xs[s] = x8{};
     }
+  }
+
+  if constexpr (!RING_FIRST) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(wr + ws * u));
   }
 
   // one block's k-steps; LAST: the workgroup's final block, whose last U
   // slots are not refilled (a one-block workgroup would otherwise fetch U of
   // its STEPS k-steps twice)
+  struct Acc {
+    f4 v[MB];
+  };
   auto run_block = [&](auto last_c) {
     constexpr bool LAST = decltype(last_c)::value;
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    Acc acc;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc.v[mb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
-      acc = mfma16x16x32<T>(a[s % U], xs[s], acc);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc.v[mb] = mfma16x16x32<T>(a[s % U], xs[mb][s], acc.v[mb]);
       if (!LAST || s + U < STEPS) {
         const T* src = s + U < STEPS ? wr + ws * (s + U) : wn + wsn * (s + U - STEPS);
         a[s % U] = __builtin_nontemporal_load(reinterpret_cast<const x8*>(src));
@@ -458,19 +527,26 @@ __global__ __launch_bounds__(512) void skinny_pgemm_k(const SkinnyArgs p) {
   };
   for (;; ++j) {
     const bool last = j + 1 >= nunits;
-    const f4 acc = last ? run_block(std::true_type{}) : run_block(std::false_type{});
-    part[j & 1][wave][lane] = acc;
+    const Acc acc = last ? run_block(std::true_type{}) : run_block(std::false_type{});
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) part[j & 1][wave][mb][lane] = acc.v[mb];
     __syncthreads();
     if (wave == 0) {
-      f4 t = part[j & 1][0][lane];
 #pragma unroll
-      for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][lane];  // fixed order
-      epilogue<T, EPI, ACT>(p, blk, t, lane, half, &pre);
+      for (int mb = 0; mb < MB; ++mb) {
+        f4 t = part[j & 1][0][mb][lane];
+#pragma unroll
+        for (int i = 1; i < WAVES; ++i) t += part[j & 1][i][mb][lane];  // fixed order
+        epilogue<T, EPI, ACT>(p, blk, t, lane, half, pre[mb], true, 16 * mb);
+      }
     }
     if (last) break;
     blk = unit_blk(j + 1);
     half = unit_half(j + 1);
-    if (wave == 0) epi_prefetch<T, EPI>(p, blk, lane, pre);  // lands during the block's k-loop
+    if (wave == 0) {  // lands during the block's k-loop
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) epi_prefetch<T, EPI>(p, blk, lane, pre[mb], 16 * mb);
+    }
     wr = wn;
     ws = wsn;
     wn = wptr(j + 2 < nunits ? j + 2 : nunits - 1);
@@ -495,14 +571,26 @@ template <typename T, int WAVES, int STEPS, bool NORM, int EPI, int ACT>
 void launch(const SkinnyArgs& p, hipStream_t s) {
   const int nblocks = EPI == EPI_GLU ? p.N / 8 : p.N / 16;
   if constexpr (STEPS == 0) {
+    if (p.M > 16) {  // 17-32 rows: two row blocks per W fragment
+      if constexpr (WAVES == 8) {
+        if (p.packed) {
+          hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, true, 2>),
+                             dim3((unsigned)nblocks), dim3(64 * WAVES), 0, s, p);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, false, 2>), dim3((unsigned)nblocks),
+                         dim3(64 * WAVES), 0, s, p);
+      return;
+    }
     if constexpr (WAVES == 8) {
       if (p.packed) {
-        hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, true>), dim3((unsigned)nblocks),
+        hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, true, 1>), dim3((unsigned)nblocks),
                            dim3(64 * WAVES), 0, s, p);
         return;
       }
     }
-    hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, false>), dim3((unsigned)nblocks),
+    hipLaunchKernelGGL((skinny_gemm_k<T, WAVES, NORM, EPI, ACT, false, 1>), dim3((unsigned)nblocks),
                        dim3(64 * WAVES), 0, s, p);
   } else {
     // ring depth (k-steps of weight loads in flight per wave): 16 (batch-1 graph decode
@@ -510,11 +598,22 @@ void launch(const SkinnyArgs& p, hipStream_t s) {
     // register-resident X fragments of K = 8192 (16 spilled 92-204 B per lane)
     constexpr int U = STEPS == 32 ? 8 : 16;
     const int g = nblocks < num_cus() ? nblocks : num_cus();
+    if constexpr (STEPS == 16) {
+      if (p.M > 16) {  // 17-32 rows: two row blocks, the ring 8 deep beside 2 x 16 X fragments
+        if (p.packed)
+          hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 8, true, 2>), dim3((unsigned)g),
+                             dim3(512), 0, s, p);
+        else
+          hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 8, false, 2>), dim3((unsigned)g),
+                             dim3(512), 0, s, p);
+        return;
+      }
+    }
     if (p.packed)
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, true>), dim3((unsigned)g),
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, true, 1>), dim3((unsigned)g),
                          dim3(512), 0, s, p);
     else
-      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, false>), dim3((unsigned)g),
+      hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, U, false, 1>), dim3((unsigned)g),
                          dim3(512), 0, s, p);
   }
 }
@@ -553,7 +652,7 @@ void dispatch(const SkinnyArgs& p, int epi, hipStream_t s) {
 
 
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return M >= 1 && M <= 16 && N % 16 == 0 && K % 128 == 0 && N > 0 && K > 0 &&
+  return M >= 1 && M <= 32 && N % 16 == 0 && K % 128 == 0 && N > 0 && K > 0 &&
          N * K < ((int64_t)1 << 40);
 }
 
@@ -575,7 +674,9 @@ void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
   // packed weights are cut for the 8-wave forms (the host checks K % 256 == 0)
   const bool w8 = (want == 8 || p.packed) && p.K % 256 == 0;
   const int steps = w8 ? p.K / 256 : 0;
-  if (persist && w8 && (steps == 16 || steps == 32)) {
+  // 17-32 rows: the persistent form holds two row blocks of X at K = 4096;
+  // at K = 8192 they run the per-block kernel
+  if (persist && w8 && (steps == 16 || (steps == 32 && p.M <= 16))) {
     if (dt == DT_BF16) steps == 16 ? dispatch<bf16, 8, 16>(p, epi, s) : dispatch<bf16, 8, 32>(p, epi, s);
     else steps == 16 ? dispatch<fp16, 8, 16>(p, epi, s) : dispatch<fp16, 8, 32>(p, epi, s);
     return;

@@ -31,7 +31,7 @@ from ..parallel.buffers import divide, make_viewless_tensor
 from ..parallel import tensor as tp
 from ..ops.dropout import bias_dropout_add
 from ..utils.trace import trace_range, tracing
-from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync
+from ..ops.norms import RMSNorm, MixedFusedLayerNorm, _param_sync, rms_norm
 from ..ops.rope import rope_table, apply_rope_ref, rope_qkv_inplace, rope_qkv
 from ..ops._ext import use_native, ext
 from ..parallel.context import chunk_position_ids, ring_attention
@@ -44,7 +44,7 @@ from .module import MegatronModule
 from .utils import attention_mask_func, erf_gelu
 
 
-# Decode steps (one new token per sequence, <= 16 sequences, TP = 1) run each
+# Decode steps (one new token per sequence, <= 32 sequences, any TP) run each
 # layer as 5 weight-streaming launches with the elementwise work fused in
 # (csrc/skinny_gemm.hip): [RMSNorm + QKV + RoPE + KV-cache write] ->
 # decode attention -> [dense + residual] -> [RMSNorm + fc1 + GLU] ->
@@ -107,7 +107,7 @@ class ParallelMLP(MegatronModule):
         if not self.glu_activation or self.use_bias:
             return False
         if not torch.is_grad_enabled() and x.numel() // x.shape[-1] < 256:
-            # decode rows: the weight-streaming skinny GEMM (<= 16 rows) or
+            # decode rows: the weight-streaming skinny GEMM (<= 32 rows) or
             # hipBLASLt's narrow tiles; the NT kernel's 256-row tiles would run
             # mostly empty (batch-32 decode 5.7k -> 4.5k tok/s with them)
             return False
@@ -469,7 +469,7 @@ class ParallelTransformerLayer(MegatronModule):
         no sequence parallelism: a decode step has one row per sequence)."""
         if not (_DECODE_FUSED and ip is not None and not torch.is_grad_enabled()
                 and hidden_states.is_cuda and hidden_states.dim() == 3
-                and hidden_states.shape[0] == 1 and hidden_states.shape[1] <= 16
+                and hidden_states.shape[0] == 1 and hidden_states.shape[1] <= 32
                 and hidden_states.dtype in (torch.bfloat16, torch.float16)
                 and self._fused_residual_ok()):
             return False
@@ -523,7 +523,13 @@ class ParallelTransformerLayer(MegatronModule):
         pq, po = decode_pack.packed(wq), decode_pack.packed(wo)
         tail = C.skinny_glu_half_tail(w1.shape[0] // 2, w1.shape[1], True)
         p1, p2 = decode_pack.packed(w1, glu=True, half_tail=tail), decode_pack.packed(w2)
-        q = C.skinny_qkv_rope_cache(x, wq if pq is None else pq, ln1.weight, ln1.eps, ng, r, hd,
+        # 17-32 rows: the norm runs as its own kernel and the projections take
+        # the un-normed two-row-block forms (the normed ones spill their 2 x 16
+        # X fragments: profiles/r4ai_skinny_mb.txt)
+        sep = b > 16
+        xq = rms_norm(x, ln1.weight, ln1.eps) if sep else x
+        q = C.skinny_qkv_rope_cache(xq, wq if pq is None else pq, None if sep else ln1.weight,
+                                    ln1.eps, ng, r, hd,
                                     cos, sin, pos, kc, vc,
                                     ip.device_offset if graph else None, 0 if graph else s0,
                                     pq is not None)
@@ -544,7 +550,8 @@ class ParallelTransformerLayer(MegatronModule):
         h2 = C.skinny_norm_gemm(o.reshape(b, -1), wo if po is None else po, None, 0.0,
                                 x if first else None, po is not None)
         h2 = tp.reduce_from_tensor_model_parallel_region(h2)
-        y = C.skinny_norm_glu(h2, w1 if p1 is None else p1, ln2.weight, ln2.eps,
+        y = C.skinny_norm_glu(rms_norm(h2, ln2.weight, ln2.eps) if sep else h2,
+                              w1 if p1 is None else p1, None if sep else ln2.weight, ln2.eps,
                               tp.layers._GLU_KIND[mlp.glu_activation], p1 is not None, tail)
         h3 = C.skinny_norm_gemm(y, w2 if p2 is None else p2, None, 0.0, h2 if first else None,
                                 p2 is not None)

@@ -1,6 +1,6 @@
 """Decode-packed weight layout for the weight-streaming skinny GEMM.
 
-A decode step multiplies <= 16 rows by every weight of the model, so its time
+A decode step multiplies <= 32 rows by every weight of the model, so its time
 is the weight stream from HBM (reference: ``megatron/text_generation/
 generation.py:179-264`` runs the same step through the training GEMMs).  The
 skinny kernel (``csrc/skinny_gemm.hip``) feeds ``v_mfma_f32_16x16x32`` with

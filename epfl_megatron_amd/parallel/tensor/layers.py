@@ -755,7 +755,7 @@ def glu_mlp(input_, w1, w2, glu_kind, *, sequence_parallel, tp_async_allreduce,
                            tp_async_allreduce, gradient_accumulation_fusion)
 
 
-# Decode-sized inference batches (<= 16 token rows, no autograd): the weight-
+# Decode-sized inference batches (<= 32 token rows, no autograd): the weight-
 # streaming HIP GEMM (csrc/skinny_gemm.hip) instead of hipBLASLt's skinny
 # tiles (profiles/r2c_skinny_gemm.txt).  EMA_SKINNY_GEMM=0 disables it.
 _SKINNY = os.environ.get("EMA_SKINNY_GEMM", "1") != "0"
@@ -769,7 +769,7 @@ def _skinny_linear(input_, weight, bias, sequence_parallel):
     k = input_.shape[-1]
     m = input_.numel() // k
     n = weight.shape[0]
-    if m > 16 or not weight.is_contiguous() or not ext().skinny_gemm_supported(m, n, k):
+    if m > 32 or not weight.is_contiguous() or not ext().skinny_gemm_supported(m, n, k):
         return None
     # K = 4096 / 8192 run the persistent skinny kernel, faster than hipBLASLt up
     # to the LM head at 16 rows; the per-block form loses to hipBLASLt's wide

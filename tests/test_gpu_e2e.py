@@ -156,7 +156,7 @@ def test_gpu_kv_cached_decode_matches_full_forward():
     assert err < 3e-2 * max(1.0, scale), (err, scale)
 
 
-def _decode_fused_vs_unfused(rank, world):
+def _decode_fused_vs_unfused(rank, world, b=3):
     """The fused decode layer (5 weight-streaming launches with norm / RoPE /
     KV-cache write / GLU / residual inside, csrc/skinny_gemm.hip) against the
     unfused kernels on the same prefilled cache: logits and greedy tokens."""
@@ -178,7 +178,7 @@ def _decode_fused_vs_unfused(rank, world):
         return orig(self, *a, **k)
     transformer.ParallelTransformerLayer._forward_decode_fused = counted
     torch.manual_seed(6)
-    b, plen, n = 3, 21, 8
+    plen, n = 21, 8
     prompt = torch.randint(0, 512, (b, plen), device="cuda")
     pos = torch.arange(plen + n, device="cuda")[None].expand(b, -1)
     runs = {}
@@ -208,11 +208,17 @@ def _decode_fused_vs_unfused(rank, world):
 
 
 @pytest.mark.gpu
-def test_gpu_fused_decode_matches_unfused():
-    calls, err, scale, tf, tu, cache_err = run_dist(_decode_fused_vs_unfused, 1)[0]
+@pytest.mark.parametrize("b", [3, 24])
+def test_gpu_fused_decode_matches_unfused(b):
+    """b = 24: 17-32 sequences run two 16-row blocks per weight fragment."""
+    calls, err, scale, tf, tu, cache_err = run_dist(_decode_fused_vs_unfused, 1, b)[0]
     assert calls == 2 * 8, calls  # every decode step of both layers took the fused path
     assert err < 2e-2 * max(1.0, scale), (err, scale)
-    assert tf == tu
+    if b <= 16:
+        assert tf == tu
+    else:  # (24 x 8 greedy picks through two numerics paths: allow rare near-tie flips)
+        same = sum(x == y for a, c in zip(tf, tu) for x, y in zip(a, c))
+        assert same >= 0.9 * b * 8, (same, tf, tu)
     assert cache_err < 5e-2, cache_err
 
 
@@ -299,15 +305,20 @@ def test_gpu_generation_api_hip_graph_matches_eager():
         assert a == pytest.approx(b, abs=1e-2)
 
 
-def _decode_tp(rank, world, fused):
+def _decode_tp(rank, world, fused, xgmi_kb=0):
     """KV-cached greedy decode of the tiny GQA Llama at TP = world on one GPU
     (gloo collectives on cuda tensors: RCCL refuses two ranks on one device),
-    through the fused decode layer (``fused``) or the unfused kernels.
-    Returns the full-vocabulary decode logits and tokens."""
+    through the fused decode layer (``fused``) or the unfused kernels; with
+    ``xgmi_kb`` the TP all-reduces of at most that many KiB take the one-shot
+    peer-memory kernel (parallel/xgmi.py).  Returns the full-vocabulary decode
+    logits and tokens (and, with ``xgmi_kb``, the one-shot call count)."""
     import torch.distributed as dist
     import finetune
-    init_framework(LLAMA_GQA + ["--bf16", "--tensor_model_parallel_size", str(world)],
+    extra = ["--tp_xgmi_allreduce_kb", str(xgmi_kb)] if xgmi_kb else []
+    init_framework(LLAMA_GQA + ["--bf16", "--tensor_model_parallel_size", str(world)] + extra,
                    finetune.extra_args)
+    from epfl_megatron_amd.parallel import comm as _comm
+    _comm.report(reset=True)
     from epfl_megatron_amd import get_args
     from epfl_megatron_amd.models import ModelType, transformer
     from epfl_megatron_amd.training import get_model
@@ -349,7 +360,32 @@ def _decode_tp(rank, world, fused):
             ip.sequence_len_offset += 1
     transformer._DECODE_FUSED = True
     transformer.ParallelTransformerLayer._forward_decode_fused = orig
+    if xgmi_kb:
+        xg = _comm.xgmi_allreduce_of(state.get_tensor_model_parallel_group())
+        xg.check()
+        n_one = sum(v[0] for k, v in _comm.report().items() if k.startswith("all_reduce_xgmi"))
+        _comm.enable_xgmi_allreduce(state.get_tensor_model_parallel_group(), 0)
+        return n_one, torch.cat(logits, 1), torch.cat(toks, 1).tolist()
     return calls[0], torch.cat(logits, 1), torch.cat(toks, 1).tolist()
+
+
+@pytest.mark.gpu
+def test_gpu_fused_decode_tensor_parallel_xgmi_oneshot():
+    """TP=2 fused decode with the decode all-reduces on the one-shot
+    peer-memory kernel (two ranks sharing the GPU through IPC mappings) equals
+    the same decode on process-group all-reduces."""
+    n_one, lx, tx = run_dist(_decode_tp, 2, True, 64, env={"LOCAL_RANK": "0"})[0]
+    _, lg, tg = run_dist(_decode_tp, 2, True, env={"LOCAL_RANK": "0"})[0]
+    # 2 row-parallel all-reduces per layer per decode step (+ the prefill's)
+    assert n_one >= 2 * 2 * 6, n_one
+    # (same fp32-then-round sum of two ranks; gloo's bf16 reduction may round
+    # differently in rare cases, so a bf16-level tolerance and near-tie tokens)
+    tol = 3e-2 * max(1.0, float(lg.abs().max()))
+    assert float((lx - lg).abs().max()) < tol
+    for i, (ra, rb) in enumerate(zip(tg, tx)):
+        for j, (a, bb) in enumerate(zip(ra, rb)):
+            if a != bb:
+                assert abs(float(lg[i, j, a] - lg[i, j, bb])) < 2 * tol, (i, j, a, bb)
 
 
 @pytest.mark.gpu

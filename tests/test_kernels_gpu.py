@@ -469,7 +469,8 @@ def test_flash_decode(b, sk, nq, nkv, hd):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (5, 12288, 4096), (16, 4096, 11008),
-                                   (4, 32000, 4096), (3, 1376, 512)])
+                                   (4, 32000, 4096), (3, 1376, 512), (24, 4096, 4096),
+                                   (32, 4096, 11008), (17, 1376, 512)])
 def test_skinny_gemm(M, N, K):
     """Decode-batch weight-streaming GEMM vs fp32 reference, and the linear
     layers' no-grad dispatch to it."""
@@ -480,7 +481,7 @@ def test_skinny_gemm(M, N, K):
     assert C.skinny_gemm_supported(M, N, K)
     y = C.skinny_gemm(x, w)
     _close(y, x.float() @ w.float().t(), 2e-2, 2e-2, "skinny gemm")
-    assert not C.skinny_gemm_supported(17, N, K) and not C.skinny_gemm_supported(M, N, K + 64)
+    assert not C.skinny_gemm_supported(33, N, K) and not C.skinny_gemm_supported(M, N, K + 64)
     from epfl_megatron_amd.parallel.tensor.layers import _skinny_linear
     with torch.no_grad():
         y2 = _skinny_linear(x.view(M, 1, K), w, None, False)
@@ -488,7 +489,8 @@ def test_skinny_gemm(M, N, K):
     assert _skinny_linear(x.view(M, 1, K), w, None, False) is None  # grad mode on: autograd path
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 1024, 512), (16, 4096, 11008), (3, 512, 384)])
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 1024, 512), (16, 4096, 11008), (3, 512, 384),
+                                   (32, 4096, 4096), (19, 1024, 512)])
 def test_skinny_fused_norm_residual(M, N, K):
     """Decode projection with the RMSNorm prologue and the residual epilogue
     vs the unfused kernels (rmsnorm_fwd -> skinny GEMM -> add, same roundings)."""
@@ -513,7 +515,8 @@ def test_skinny_fused_norm_residual(M, N, K):
 
 @pytest.mark.parametrize("kind,name", [(0, "swiglu"), (1, "geglu")])
 @pytest.mark.parametrize("M,F,K", [(1, 11008, 4096), (8, 512, 512), (16, 1376, 4096),
-                                   (3, 2816, 4096), (5, 5632, 4096)])
+                                   (3, 2816, 4096), (5, 5632, 4096), (32, 1376, 4096),
+                                   (24, 512, 512)])
 def test_skinny_fused_glu(M, F, K, kind, name):
     """fc1 decode projection with the norm prologue and the GLU epilogue vs
     rmsnorm -> skinny GEMM -> glu kernel.  F = 11008 / 2816 on 256 CUs run
@@ -570,7 +573,8 @@ def test_skinny_fused_qkv_rope_cache(ng, r, hd, graph_slot):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 12288, 4096), (16, 4096, 11008),
-                                   (3, 1024, 8192), (5, 512, 512), (1, 22016, 4096)])
+                                   (3, 1024, 8192), (5, 512, 512), (1, 22016, 4096),
+                                   (32, 12288, 4096), (20, 4096, 11008)])
 def test_skinny_packed_weights_match_row_major(M, N, K):
     """The decode-packed weight layout (ops/decode_pack.py) feeds every lane
     the same k indices in the same order as the row-major stream: plain,
