@@ -238,10 +238,10 @@ FLAG_TABLE = {
               help="communicators over the DP ranks; DDP buckets are issued round-robin "
                    "on them so several reduce concurrently (one RCCL stream each)"),
         _flag("--tp_xgmi_allreduce_kb", type=int, default=0,
-              help="route tensor-parallel sum all-reduces of at most this many KiB "
-                   "(contiguous, 16-B sized) through the one-shot xGMI peer-memory kernel "
-                   "(parallel/xgmi.py) instead of RCCL; 0 = off.  For the latency-bound "
-                   "[b, h] all-reduces of TP decode"),
+              help="route tensor-parallel sum all-reduces and all-gathers of at most this "
+                   "many KiB per rank (contiguous, 16-B sized) through the one-shot xGMI "
+                   "peer-memory kernel (parallel/xgmi.py) instead of RCCL; 0 = off.  For the "
+                   "latency-bound [b, h] all-reduces and logits all-gathers of TP decode"),
         _flag("--no_overlap_grad_reduce", action="store_false", dest="overlap_grad_reduce"),
         _flag("--no_overlap_param_gather", action="store_false", dest="overlap_param_gather",
               help="dist-opt: all-gather parameters synchronously at step end instead of "

@@ -1171,6 +1171,28 @@ void xgmi_all_reduce(int64_t id, const at::Tensor& inp, at::Tensor out) {
   ema::xgmi_all_reduce(id, inp.data_ptr(), out.data_ptr(), nbytes, dt, cur_stream());
 }
 
+void xgmi_all_gather(int64_t id, const at::Tensor& inp, at::Tensor out, int64_t world) {
+  check_gpu(inp, "inp");
+  check_gpu(out, "out");
+  const int dt = dtype_code(inp);
+  TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16 || dt == ema::DT_F32, "xgmi_all_gather: dtype");
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == world * inp.numel() &&
+                  inp.is_contiguous() && out.is_contiguous(),
+              "xgmi_all_gather: contiguous in [n] / out [world * n] of one dtype");
+  const int64_t nbytes = inp.numel() * inp.element_size();
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(inp.data_ptr()),
+                  ob = reinterpret_cast<uintptr_t>(out.data_ptr());
+  // in disjoint from out, or exactly one of its chunks (the in-place form: every
+  // element of in is read and then overwritten by the same thread)
+  const bool chunk_alias = ib >= ob && ib < ob + world * nbytes && (ib - ob) % nbytes == 0;
+  TORCH_CHECK(ib + nbytes <= ob || ob + world * nbytes <= ib || chunk_alias,
+              "xgmi_all_gather: in must be disjoint from out or one of its chunks");
+  TORCH_CHECK(nbytes % 16 == 0 && ib % 16 == 0 && ob % 16 == 0,
+              "xgmi_all_gather: 16-byte aligned, 16-byte sized buffers");
+  TORCH_CHECK(nbytes <= ema::xgmi_capacity(id), "xgmi_all_gather: message exceeds the registered capacity");
+  ema::xgmi_all_gather(id, inp.data_ptr(), out.data_ptr(), nbytes, dt, cur_stream());
+}
+
 void register_gemm_lt(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1245,6 +1267,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_create", &xgmi_create);
   m.def("xgmi_open", &xgmi_open);
   m.def("xgmi_all_reduce", &xgmi_all_reduce);
+  m.def("xgmi_all_gather", &xgmi_all_gather);
   m.def("xgmi_error", [](int64_t id) { return ema::xgmi_error(id); });
   m.def("xgmi_destroy", [](int64_t id) { ema::xgmi_destroy(id); });
   m.def("flash_decode", &flash_decode, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"),

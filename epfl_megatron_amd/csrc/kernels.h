@@ -222,6 +222,8 @@ int xgmi_handle_size();
 void xgmi_open(int64_t id, const void* handles);
 int64_t xgmi_capacity(int64_t id);
 void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s);
+// out [world * nbytes] = every rank's in [nbytes], rank-major (in: disjoint or one chunk of out)
+void xgmi_all_gather(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s);
 int xgmi_error(int64_t id);
 void xgmi_destroy(int64_t id);
 

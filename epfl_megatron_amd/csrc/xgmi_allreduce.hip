@@ -1,4 +1,5 @@
-// One-shot all-reduce over xGMI peer memory for small, latency-bound messages
+// One-shot all-reduce / all-gather over xGMI peer memory for small,
+// latency-bound messages
 // (the TP all-reduces of a decode step are [b, h] = a few KiB,
 // where a ring collective's 2(W-1) link hops and its launch / proxy overhead
 // dominate).  RCCL stays the default and the fallback (parallel/comm.py routes
@@ -55,7 +56,9 @@ struct XgArgs {
   int rank, world;
 };
 
-template <typename T>
+// GATHER: out[p * nbytes + off] = rank p's chunk (all-gather along dim 0)
+// instead of the rank-ordered sum; same transport, flags and parities.
+template <typename T, bool GATHER>
 __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int64_t off = (int64_t)b * XG_CHUNK + (int64_t)t * 16;
@@ -89,7 +92,12 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  if (valid) {
+  if (GATHER) {
+    if (valid)
+      for (int p = 0; p < a.world; ++p)
+        st16(reinterpret_cast<T*>(a.out + (int64_t)p * a.nbytes + off),
+             ld16(reinterpret_cast<const T*>(a.data[a.rank] + par + (int64_t)p * a.cap + off)));
+  } else if (valid) {
     constexpr int N = V16<T>::N;
     float acc[N];
 #pragma unroll
@@ -175,7 +183,8 @@ void xgmi_open(int64_t id, const void* handles) {
 
 int64_t xgmi_capacity(int64_t id) { return get(id)->cap; }
 
-void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s) {
+void xgmi_launch(int64_t id, const void* in, void* out, int64_t nbytes, int dt, bool gather,
+                 hipStream_t s) {
   XgComm* c = get(id);
   if (nbytes <= 0) return;
   if (nbytes > c->cap || nbytes % 16) throw std::runtime_error("xgmi: message exceeds capacity or is not 16-B sized");
@@ -196,9 +205,23 @@ void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int 
   a.rank = c->rank;
   a.world = c->world;
   const unsigned grid = (unsigned)((nbytes + XG_CHUNK - 1) / XG_CHUNK);
-  EMA_DISPATCH_FLOAT(dt, T, {
-    hipLaunchKernelGGL((xgmi_oneshot_k<T>), dim3(grid), dim3(XG_THREADS), 0, s, a);
-  });
+  if (gather) {
+    EMA_DISPATCH_FLOAT(dt, T, {
+      hipLaunchKernelGGL((xgmi_oneshot_k<T, true>), dim3(grid), dim3(XG_THREADS), 0, s, a);
+    });
+  } else {
+    EMA_DISPATCH_FLOAT(dt, T, {
+      hipLaunchKernelGGL((xgmi_oneshot_k<T, false>), dim3(grid), dim3(XG_THREADS), 0, s, a);
+    });
+  }
+}
+
+void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s) {
+  xgmi_launch(id, in, out, nbytes, dt, false, s);
+}
+
+void xgmi_all_gather(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s) {
+  xgmi_launch(id, in, out, nbytes, dt, true, s);
 }
 
 int xgmi_error(int64_t id) {

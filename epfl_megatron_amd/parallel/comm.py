@@ -78,9 +78,9 @@ def set_loopback(group, world):
 
 
 def enable_xgmi_allreduce(group, cap_bytes):
-    """Route small sum all-reduces on ``group`` (contiguous bf16 / fp16 / fp32
-    CUDA tensors of at most ``cap_bytes``) through the one-shot xGMI kernel
-    (``parallel/xgmi.py``); RCCL keeps everything else.  Collective over the
+    """Route small sum all-reduces and all-gathers on ``group`` (contiguous
+    bf16 / fp16 / fp32 CUDA tensors of at most ``cap_bytes`` per rank) through
+    the one-shot xGMI kernel (``parallel/xgmi.py``); RCCL keeps everything else.  Collective over the
     group (handle exchange).  ``cap_bytes`` 0 / None disables."""
     old = _XGMI.pop(id(group), None)
     if old is not None:
@@ -300,6 +300,11 @@ def all_gather_into(output, inp, group=None, async_op=False):
             if own.data_ptr() != src.data_ptr():
                 own.copy_(src)
         return _issue("all_gather", group, output, src, loop, async_op)
+    xg = _XGMI.get(id(group))
+    if xg is not None and xg.gather_eligible(output, src):
+        def oneshot(a):
+            xg.all_gather(output, src)
+        return _issue("all_gather_xgmi", group, output, src, oneshot, async_op)
     return _issue("all_gather", group, output, src,
                   lambda a: dist.all_gather_into_tensor(output, src, group=group, async_op=a),
                   async_op)

@@ -1,4 +1,4 @@
-"""One-shot all-reduce over xGMI peer memory (``csrc/xgmi_allreduce.hip``).
+"""One-shot all-reduce / all-gather over xGMI peer memory (``csrc/xgmi_allreduce.hip``).
 
 SURVEY §5.8 ("a custom one-shot all-reduce / all-gather kernel over xGMI peer
 memory (IPC handles) for small, latency-bound messages ... RCCL stays the
@@ -19,7 +19,9 @@ Use: ``comm.enable_xgmi_allreduce(group, cap_bytes)`` (``--tp_xgmi_allreduce_kb`
 does it for the TP group at initialisation); ``comm.all_reduce`` then routes
 sum all-reduces of contiguous bf16 / fp16 / fp32 CUDA tensors of at most
 ``cap_bytes`` (16-byte sized and aligned) on that group here, everything else
-to RCCL.  Capturable in a hipGraph (epochs live on the device).
+to RCCL, and ``comm.all_gather_into`` likewise the all-gathers whose
+per-rank message fits (e.g. the vocab-parallel decode logits).  Capturable in
+a hipGraph (epochs live on the device).
 
 Verified on one MI355X with 2 and 4 processes sharing the GPU
 (``tests/test_xgmi_gpu.py``: same-device IPC mappings; the flag / parity
@@ -74,6 +76,16 @@ class XgmiAllReduce:
         the current stream."""
         _ext().xgmi_all_reduce(self.id, t, t if out is None else out)
         return t if out is None else out
+
+    def gather_eligible(self, out, inp):
+        return (self.eligible(inp) and out.is_cuda and out.dtype == inp.dtype and out.is_contiguous()
+                and out.numel() == self.world * inp.numel() and out.data_ptr() % 16 == 0)
+
+    def all_gather(self, out, inp):
+        """``out`` = concat over ranks of ``inp`` along dim 0 (``inp`` may be
+        this rank's chunk of ``out``), on the current stream."""
+        _ext().xgmi_all_gather(self.id, inp, out, self.world)
+        return out
 
     def check(self):
         """Raise if a wait timed out (a peer never arrived); synchronises."""

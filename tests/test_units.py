@@ -482,6 +482,14 @@ class _FakeOneShot:
         dist.all_reduce(t, group=self.group)
         return t
 
+    def gather_eligible(self, out, inp):
+        return self.eligible(inp)
+
+    def all_gather(self, out, inp):
+        self.calls += 1
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+        return out
+
 
 def _oneshot_routing(rank, world):
     from epfl_megatron_amd.parallel import comm
@@ -498,18 +506,24 @@ def _oneshot_routing(rank, world):
     comm.all_reduce(mx, group=grp, op="max")
     w = comm.all_reduce(small, group=grp, async_op=True)
     w.wait()
+    g_small = torch.empty(world * 4)
+    comm.all_gather_into(g_small, torch.full((4,), float(rank)), group=grp)   # one-shot
+    g_big = torch.empty(world * 32)
+    comm.all_gather_into(g_big, torch.full((32,), float(rank)), group=grp)    # process group
     rep = comm.report()
     comm._XGMI.pop(id(grp))
+    assert g_small.tolist() == [float(r) for r in range(world) for _ in range(4)]
+    assert g_big.tolist() == [float(r) for r in range(world) for _ in range(32)]
     return fake.calls, sorted(k.split("/")[0] for k in rep), small[0].item(), big[0].item(), mx[0].item()
 
 
 def test_xgmi_oneshot_routing_cpu():
-    """comm.all_reduce sends eligible sum all-reduces of a registered group to
-    the one-shot communicator (accounted as all_reduce_xgmi) and everything
-    else to the process group."""
+    """comm.all_reduce / all_gather_into send eligible sum all-reduces and
+    all-gathers of a registered group to the one-shot communicator (accounted
+    as *_xgmi) and everything else to the process group."""
     for calls, keys, s, b, m in run_dist(_oneshot_routing, 2):
-        assert calls == 2
-        assert keys == ["all_reduce", "all_reduce_xgmi"]
+        assert calls == 3
+        assert keys == ["all_gather", "all_gather_xgmi", "all_reduce", "all_reduce_xgmi"]
         assert s == 6.0 and b == 3.0 and m == 1.0
 
 

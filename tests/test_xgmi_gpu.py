@@ -1,4 +1,4 @@
-"""One-shot xGMI all-reduce (csrc/xgmi_allreduce.hip, parallel/xgmi.py).
+"""One-shot xGMI all-reduce / all-gather (csrc/xgmi_allreduce.hip, parallel/xgmi.py).
 
 Several processes share the one GPU of the test box: each maps the others'
 regions through same-device IPC handles, so the flag / parity protocol and the
@@ -55,6 +55,22 @@ def _rank(rank, world):
                 if not torch.equal(got.cpu(), _oracle(xs)):
                     bad.append((it, str(dt), n))
     xg.check()
+    # all-gather (rank-major along dim 0): out of place and in place
+    for it in range(6):
+        for dt in DTYPES:
+            n = (8, 2048 + 8, 40000)[it % 3]
+            xs = _inputs(world, n, dt, 500 + 31 * it + n)
+            ref = torch.cat(xs)
+            out = torch.empty(world * n, dtype=dt, device="cuda")
+            if it % 2:
+                out.view(world, n)[rank].copy_(xs[rank])
+                xg.all_gather(out, out.view(world, n)[rank])
+            else:
+                xg.all_gather(out, xs[rank].cuda())
+            torch.cuda.synchronize()
+            if not torch.equal(out.cpu(), ref):
+                bad.append(("gather", it, str(dt), n))
+    xg.check()
     # captured in a hipGraph: replays advance the device-side epochs
     t = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
     torch.cuda.synchronize()
@@ -101,9 +117,16 @@ def _rank(rank, world):
     comm.all_reduce(t, group=grp)
     big = torch.ones(128 * 1024, dtype=torch.float32, device="cuda")
     comm.all_reduce(big, group=grp)
+    gout = torch.empty(world * 512, dtype=torch.bfloat16, device="cuda")
+    comm.all_gather_into(gout, torch.full((512,), float(rank), dtype=torch.bfloat16, device="cuda"),
+                         group=grp)
     torch.cuda.synchronize()
     rep = comm.report()
     routed = [k for k in rep if k.startswith("all_reduce_xgmi")]
+    routed_g = [k for k in rep if k.startswith("all_gather_xgmi")]
+    gref = torch.arange(world).repeat_interleave(512).to(torch.bfloat16)
+    if not routed_g or not torch.equal(gout.cpu(), gref):
+        bad.append(("comm gather", sorted(rep)))
     if not torch.equal(t.cpu(), _oracle(xs)) or not routed or not torch.all(big == world):
         bad.append(("comm", sorted(rep)))
     comm._XGMI.pop(id(grp))
