@@ -26,8 +26,11 @@
 // epoch e before it reaches e+1), and e+1 writes the other parity.  Epochs are
 // device-side per workgroup, so the launch is hipGraph-capturable.
 //
-// The waits are bounded (a few seconds): on timeout the error word is set and the
-// kernel ends (no hang); XgmiAllReduce.check() raises on it.
+// The waits are bounded (2^25 polls, tens of seconds: TP ranks drift apart by
+// host work such as logging between collectives, so a short bound would fire
+// on healthy runs): on timeout the error word is set and the kernel ends
+// instead of hanging the GPU on a dead peer; XgmiAllReduce.check() raises on
+// it, and comm.report() (every training log interval) checks.
 #include "common.h"
 #include "kernels.h"
 
@@ -80,11 +83,11 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < a.world) {
     const unsigned* f = a.own_flags + (int64_t)b * a.world + t;
-    int spins = 0;
+    int spins = 0;  // (one poll ~1 us: uncached load + sleep)
     // (a peer may already be one epoch ahead: >= in wrap-safe form)
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 21)) {
+      if (++spins > (1 << 25)) {
         __hip_atomic_store(a.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

@@ -149,8 +149,12 @@ def _fold_events(block=False):
 
 
 def report(reset=True):
-    """{key: (count, bytes, ms)} since the last report."""
+    """{key: (count, bytes, ms)} since the last report.  Also raises if a
+    one-shot xGMI collective timed out waiting for a peer since it was set up
+    (its results would be wrong: parallel/xgmi.py)."""
     _fold_events(block=True)
+    for xg in _XGMI.values():
+        xg.check()
     out = {k: tuple(v) for k, v in _STATS.items()}
     if reset:
         _STATS.clear()

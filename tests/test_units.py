@@ -485,6 +485,9 @@ class _FakeOneShot:
     def gather_eligible(self, out, inp):
         return self.eligible(inp)
 
+    def check(self):
+        self.checked = True
+
     def all_gather(self, out, inp):
         self.calls += 1
         dist.all_gather_into_tensor(out, inp, group=self.group)
@@ -511,6 +514,7 @@ def _oneshot_routing(rank, world):
     g_big = torch.empty(world * 32)
     comm.all_gather_into(g_big, torch.full((32,), float(rank)), group=grp)    # process group
     rep = comm.report()
+    assert fake.checked  # report() checks the one-shot error word
     comm._XGMI.pop(id(grp))
     assert g_small.tolist() == [float(r) for r in range(world) for _ in range(4)]
     assert g_big.tolist() == [float(r) for r in range(world) for _ in range(32)]
