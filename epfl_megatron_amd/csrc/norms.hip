@@ -24,7 +24,10 @@ constexpr int kLdsDwMaxH = 4096;  // 4 waves x H x fp32 <= 64 KB of LDS
 // res != nullptr: the normalised input is s = x + res (rounded to T, as the
 // reference's bf16 residual add), and s is written to sum_out (the residual
 // stream for the next block) -- one pass instead of an add kernel + a norm.
-template <typename T, int VPL>
+// PREW (few rows: decode): the weight slices are loaded with x, before the
+// row reduction, so the kernel makes one memory round trip instead of two; with
+// many rows the extra registers would cost occupancy and w is L2-resident anyway.
+template <typename T, int VPL, bool PREW>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
                                                      const T* __restrict__ res,
                                                      T* __restrict__ sum_out,
@@ -37,13 +40,14 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
   if (row >= rows) return;
   const int nvec = H / N;
   const T* xr = x + row * H;
-  V16<T> xv[VPL];
+  V16<T> xv[VPL], wpre[PREW ? VPL : 1];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int vi = lane + i * 64;
     if (vi < nvec) {
       xv[i] = ld16(xr + vi * N);
+      if constexpr (PREW) wpre[i] = ld16(w + vi * N);
       if (res) {
         const V16<T> rv = ld16(res + row * H + vi * N);
 #pragma unroll
@@ -65,7 +69,9 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
   for (int i = 0; i < VPL; ++i) {
     const int vi = lane + i * 64;
     if (vi < nvec) {
-      const V16<T> wv = ld16(w + vi * N);
+      V16<T> wv;
+      if constexpr (PREW) wv = wpre[i];
+      else wv = ld16(w + vi * N);
       V16<T> o;
 #pragma unroll
       for (int e = 0; e < N; ++e) {
@@ -547,9 +553,15 @@ void rmsnorm_fwd(const void* x, const void* res, void* sum_out, const void* w, v
   const int64_t blocks = (rows + kWaves - 1) / kWaves;
   EMA_DISPATCH_FLOAT(dt, T, {
     const int vpl = pick_vpl<T>(H);
-    EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_fwd_k<T, V>), dim3(blocks), dim3(256), 0, s,
-                                           (const T*)x, (const T*)res, (T*)sum_out, (const T*)w,
-                                           (T*)y, rstd, rows, H, eps));
+    if (rows <= 64 && vpl <= 8) {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_fwd_k<T, V, true>), dim3(blocks), dim3(256), 0,
+                                             s, (const T*)x, (const T*)res, (T*)sum_out,
+                                             (const T*)w, (T*)y, rstd, rows, H, eps));
+    } else {
+      EMA_VPL_SWITCH(vpl, hipLaunchKernelGGL((rmsnorm_fwd_k<T, V, false>), dim3(blocks), dim3(256), 0,
+                                             s, (const T*)x, (const T*)res, (T*)sum_out,
+                                             (const T*)w, (T*)y, rstd, rows, H, eps));
+    }
   });
 }
 
