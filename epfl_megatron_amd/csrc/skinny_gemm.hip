@@ -196,7 +196,10 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_k(const SkinnyArgs p) 
   typedef typename fa::MT<T>::x8 x8;
   // (a 16-deep ring for one row block measured the same: fc2 K = 11008 at
   // 16 rows 23.2 vs 23.0 us, profiles/r4al_skinny_u16.txt)
-  constexpr int U = SKINNY_U;
+  // two un-normed row blocks (fc2 at 17-32 rows, K = 11008: 43 k-steps per
+  // wave = 3 x 14 + 1): 14 deep, 28.6 / 33.4 us at 24 / 32 rows vs 29.7 / 34.8
+  // at 8 (profiles/r4ar_skinny_u14.txt)
+  constexpr int U = MB == 2 && !NORM ? 14 : SKINNY_U;
   __shared__ f4 part[WAVES][MB][64];
   __shared__ float ssq[WAVES][16 * MB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
