@@ -604,7 +604,10 @@ void launch(const SkinnyArgs& p, hipStream_t s) {
     constexpr int U = STEPS == 32 ? 8 : 16;
     const int g = nblocks < num_cus() ? nblocks : num_cus();
     if constexpr (STEPS == 16) {
-      if (p.M > 16) {  // 17-32 rows: two row blocks, the ring 8 deep beside 2 x 16 X fragments
+      // 17-32 rows: two row blocks, the ring 8 deep beside 2 x 16 X fragments
+      // (16 deep for the un-normed forms measured within noise: o_proj 13.6 /
+      // 14.5 vs 13.0 / 14.3 us at 24 / 32 rows, profiles/r4as_pskinny_u16.txt)
+      if (p.M > 16) {
         if (p.packed)
           hipLaunchKernelGGL((skinny_pgemm_k<T, NORM, EPI, ACT, STEPS, 8, true, 2>), dim3((unsigned)g),
                              dim3(512), 0, s, p);
