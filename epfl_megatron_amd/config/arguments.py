@@ -9,6 +9,7 @@ plus MI355X-specific additions (bucket sizes, synthetic data, kernel knobs).
 """
 
 import argparse
+import warnings
 import os
 
 import torch
@@ -81,8 +82,10 @@ FLAG_TABLE = {
         _flag("--log_params_norm", action="store_true"),
         _flag("--log_num_zeros_in_grad", action="store_true"),
         _flag("--timing_log_level", type=int, default=0, choices=range(0, 3)),
-        _flag("--no_barrier_with_level_1_timing", action="store_false",
-              dest="barrier_with_L1_time"),
+        # reference spelling (megatron/arguments.py:492, store_false: passing it
+        # turns the level-1 timer barriers OFF); the descriptive name is an alias
+        _flag(("--barrier_with_L1_time", "--no_barrier_with_level_1_timing"),
+              action="store_false", dest="barrier_with_L1_time"),
         _flag("--timing_log_option", type=str, default="minmax",
               choices=["max", "minmax", "all"]),
         _flag("--tensorboard_log_interval", type=int, default=1),
@@ -345,7 +348,8 @@ def build_base_parser():
     for section, flags in FLAG_TABLE.items():
         group = parser.add_argument_group(title=section)
         for name, kw in flags:
-            group.add_argument(name, **kw)
+            names = name if isinstance(name, tuple) else (name,)
+            group.add_argument(*names, **kw)
     return parser
 
 
@@ -536,6 +540,11 @@ def _derive_schedule_and_model(args):
 
 
 def _derive_recompute_and_parallel_features(args):
+    if getattr(args, "use_ring_exchange_p2p", False):
+        warnings.warn("--use_ring_exchange_p2p is accepted for compatibility and ignored: "
+                      "pipeline p2p always runs as batched isend/irecv over RCCL "
+                      "(parallel/pipeline/p2p.py; torch.distributed has no ring_exchange)",
+                      stacklevel=2)
     if args.distribute_saved_activations:
         _require(args.tensor_model_parallel_size > 1,
                  "can distribute recomputed activations only across tensor model parallel groups")

@@ -1201,15 +1201,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.def("wgrad_set_variant", &ema::wgrad_set_variant);
-  m.def("gemm_nt_ablation", [](const at::Tensor& a, const at::Tensor& b, at::Tensor c, int64_t mode) {
+  m.def("gemm_lab", [](const at::Tensor& a, const at::Tensor& b, at::Tensor c, int64_t variant) {
     TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
                     c.scalar_type() == at::kBFloat16 && a.is_contiguous() && b.is_contiguous() &&
                     c.is_contiguous() && a.size(1) == b.size(1) && c.size(0) == a.size(0) &&
                     c.size(1) == b.size(0) && a.size(1) % 64 == 0 && a.size(1) >= 128 &&
                     b.size(0) % 8 == 0,
-                "gemm_nt_ablation: contiguous bf16 [M,K] x [N,K] -> [M,N], K % 64 == 0, K >= 128");
-    ema::gemm_nt_ablation(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.size(0), b.size(0), a.size(1),
-                          (int)mode, cur_stream());
+                "gemm_lab: contiguous bf16 [M,K] x [N,K] -> [M,N], K % 64 == 0, K >= 128");
+    TORCH_CHECK(a.size(0) * a.size(1) * 2 < (int64_t(1) << 31) && b.size(0) * b.size(1) * 2 < (int64_t(1) << 31),
+                "gemm_lab: operands must be < 2 GiB (32-bit buffer offsets)");
+    ema::gemm_lab(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.size(0), b.size(0), a.size(1),
+                  (int)variant, cur_stream());
   });
   m.def("wgrad_plan", &wgrad_plan);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none(),

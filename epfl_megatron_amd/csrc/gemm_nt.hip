@@ -829,13 +829,9 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
   }
 }
 
-template <typename T, int EPI, int ACT, int MODE = 0>
+template <typename T, int EPI, int ACT>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
-  // MODE (ablation builds, gemm_nt_ablation): 1 = no DMA in the K-loop,
-  // 2 = neither DMA nor fragment reads (MFMA + barriers + epilogue only),
-  // 3 = DMA of the same (L2-resident) K-step every time, 4 = next-step wait
-  // 3 groups later, 5 = two DMA pieces per group, 7 = the same global reads
-  // into registers (no LDS write), 9 = A pieces only
+  // (ablation builds of this structure: gemm_lab.hip, bench-only)
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   const int lane = threadIdx.x & 63;
@@ -848,12 +844,12 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   const int M = p.M, N = p.N;
   const int nt = p.K / BK2;  // >= 2 (host-checked)
 
-  // per-lane DMA byte offsets inside a tile (fixed for the whole kernel)
+  // per-lane DMA byte offsets inside a tile (fixed for the whole kernel);
+  // piece i of the 4 waves = 32 consecutive rows (+1-3 %, profiles/r4h_gemm_ablation.txt)
   uint32_t off[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int pb = (MODE == 0 || MODE >= 15) ? 4 * i + wave : 8 * wave + i;  // 8-row block of piece i
-    // (piece i of the 4 waves = 32 consecutive rows: +1-3 %, profiles/r4h_gemm_ablation.txt)
+    const int pb = 4 * i + wave;  // 8-row block of piece i
     const int tr = 8 * pb + (lane >> 3);
     const int c = (lane & 7) ^ ((tr >> 1) & 7);
     off[i] = (uint32_t)(tr * p.lda + 8 * c) * (uint32_t)sizeof(T);
@@ -890,14 +886,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   };
   char* const ldsp = lds;
   auto dma = [&](int q, Rsrc r, uint32_t soff, int slot) {
-    if constexpr (MODE == 1 || MODE == 2) return;
-    if constexpr (MODE == 9) { if (q >= 8) return; }  // A pieces only
-    if constexpr (MODE == 7) {  // same global reads into a scratch VGPR: no LDS write
-      uint4 d;
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(off[q]), "s"(r), "s"(soff) : "memory");
-      return;
-    }
-    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + ((MODE == 0 || MODE >= 15) ? 4 * (q & 7) + wave : 8 * wave + (q & 7)) * 1024;
+    const int dst = slot * SLOTB2 + (q >= 8 ? OPB2 : 0) + (4 * (q & 7) + wave) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, off[q], soff, 0, 0);
   };
@@ -914,21 +903,12 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   }
   X8 set0[16], set1[16];
   auto read_frag = [&](X8 (&dst)[16], auto f, auto kh, uint32_t so) {
-    if constexpr (MODE == 2) return;
     constexpr int F = decltype(f)::value, KH = decltype(kh)::value;
     if constexpr (F < 8) dst[F] = row_read_imm<2048 * F, T>(abase[KH] + so);
     else dst[F] = row_read_imm<2048 * (F - 8), T>(bbase[KH] + so);
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
-  auto mfma4 = [&](X8 (&cur)[16], auto g, auto zero) {
-    constexpr int GG = decltype(g)::value;
-    static_for<4>([&](auto q) {
-      constexpr int IDX = 4 * GG + decltype(q)::value, I = IDX / 8, J = IDX % 8;
-      if constexpr (decltype(zero)::value) mfma_acc0<T>(acc[I][J], cur[8 + J], cur[I]);
-      else mfma_acc<T>(acc[I][J], cur[8 + J], cur[I]);
-    });
-  };
 
   Rsrc ra_c, rb_c, ra_n, rb_n;  // current / next tile
   make_rsrc(0, ra_c, rb_c);
@@ -951,115 +931,54 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       // source of K-step t+2: this tile, else the next tile's step t+2-nt
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
-      const uint32_t soff = MODE == 3 ? 0u : (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
-      // Schedule (per K-step, groups of 4 MFMAs): A DMA piece k at group
-      // GA + SA k, B piece k at GB + SB k, the step-t+1 wait at group WG with
-      // vmcnt = the pieces issued up to and including WG.  The production
-      // schedule (MODE 0) spreads the 16 pieces over groups 6-27: the per-CU
-      // L2 -> LDS fill path saturates when the 4 waves' pieces come in one
-      // burst (ablation modes: profiles/r4f_gemm_ablation.txt).
-      constexpr int WG = MODE == 4 ? 26 : MODE == 13 ? 25 : 23;
-      constexpr bool SPREAD = MODE == 0 || MODE == 11 || MODE == 13 || MODE == 15;
-      constexpr int GA = 6, SA = SPREAD ? 2 : MODE == 12 ? 3 : MODE == 5 ? 0 : 1;
-      constexpr int GB = SPREAD ? 13 : MODE == 12 ? 12 : MODE == 10 ? WG + 1 : 12;
-      constexpr int SB = SPREAD || MODE == 12 ? 2 : MODE == 5 ? 0 : 1;
-      auto n_upto = [](int g0, int st, int g) constexpr {
+      const uint32_t soff = (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
+      // One-MFMA slot plan (slot s = MFMA index, at most ~1 other instruction
+      // after each MFMA, the issue pattern of the vendor 256x256 kernel; +3-6 %
+      // over groups of four MFMAs, profiles/r4k_gemm_ablation.txt):
+      //   A-k-half-1 reads at 2k (k < 8), barrier 1 after slot B1, the B k-half-1
+      //   reads from B1 + 1 every 2, barrier 2 after B2, A DMA piece k at DA + SA1 k,
+      //   B piece k at DB + SB1 k (spread: the per-CU L2 -> LDS fill path stalls
+      //   on bursts, profiles/r4f_gemm_ablation.txt), the step-t+1 wait after W,
+      //   then the 16 reads of (t+1, k-half 0) spread to slot 126.
+      constexpr int B1 = 17, B2 = 35, DA = B1 + 2, SA1 = 4, DB = B2 + 2, SB1 = 8, W = 95;
+      auto cnt = [](int d, int st, int w) constexpr {
         int n = 0;
-        for (int k = 0; k < 8; ++k) n += (st == 0 ? g0 + k / 2 : g0 + st * k) <= g;
+        for (int k = 0; k < 8; ++k) n += d + st * k <= w;
         return n;
       };
-      constexpr int VM = n_upto(GA, SA, WG) + n_upto(GB, SB, WG);
-      if constexpr (MODE == 0 || MODE >= 16) {
-        // one-MFMA granularity (production schedule, MODE 0 = 16: +3-6 % over
-        // groups of four MFMAs, profiles/r4k_gemm_ablation.txt): at most ~1 other instruction after each MFMA
-        // (the issue pattern of the vendor 256x256 kernel); slots s = MFMA
-        // index.  Per-MODE slot plan: A-k-half-1 reads at 2k (k < 8), barrier 1
-        // after B1, B-k-half-1 reads from B1 + 1 every 2, barrier 2 after B2,
-        // A DMA piece k at DA + SA k, B piece k at DB + SB k, the step-t+1 wait
-        // after W, then the 16 reads of (t+1, k-half 0) spread to slot 126.
-        constexpr int B1 = MODE == 20 ? 19 : 17, B2 = MODE == 20 ? 37 : 35;
-        constexpr int DA = B1 + 2, SA1 = MODE == 17 ? 3 : 4;
-        constexpr int DB = B2 + 2, SB1 = MODE == 17 ? 6 : MODE == 19 ? 7 : 8;
-        constexpr int W = MODE == 18 ? 99 : MODE == 19 ? 97 : 95;
-        auto cnt = [](int d, int st, int w) constexpr {
-          int n = 0;
-          for (int k = 0; k < 8; ++k) n += d + st * k <= w;
-          return n;
-        };
-        constexpr int VMW = cnt(DA, SA1, W) + cnt(DB, SB1, W);
-        static_for<128>([&](auto sc) {
-          constexpr int S = decltype(sc)::value, IDX = S & 63, I = IDX / 8, J = IDX % 8;
-          if constexpr (S < 64) {
-            if constexpr (decltype(zero)::value) mfma_acc0<T>(acc[I][J], set0[8 + J], set0[I]);
-            else mfma_acc<T>(acc[I][J], set0[8 + J], set0[I]);
-          } else {
-            mfma_acc<T>(acc[I][J], set1[8 + J], set1[I]);
-          }
-          if constexpr (S < 16 && S % 2 == 0)
-            read_frag(set1, std::integral_constant<int, S / 2>{}, K1{}, so);
-          if constexpr (S == B1 || S == B2) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-          }
-          if constexpr (S > B1 && S <= B1 + 15 && (S - B1 - 1) % 2 == 0)
-            read_frag(set1, std::integral_constant<int, 8 + (S - B1 - 1) / 2>{}, K1{}, so);
-          if constexpr (S >= DA && (S - DA) % SA1 == 0 && (S - DA) / SA1 < 8)
-            dma((S - DA) / SA1, ra, soff, slot);
-          if constexpr (S >= DB && (S - DB) % SB1 == 0 && (S - DB) / SB1 < 8)
-            dma(8 + (S - DB) / SB1, rb, soff, slot);
-          if constexpr (S == W) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-          }
-          if constexpr (S > W && S < 127) {
-            // read k at slot W + 1 + floor(k (126 - W) / 16)
-            static_for<16>([&](auto kc) {
-              constexpr int Kr = decltype(kc)::value;
-              if constexpr (W + 1 + (Kr * (126 - W)) / 16 == S)
-                read_frag(set0, std::integral_constant<int, Kr>{}, K0{}, sn);
-            });
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      } else
-      static_for<32>([&](auto g) {
-        constexpr int GG = decltype(g)::value;
-        if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
-        else mfma4(set1, std::integral_constant<int, GG - 16>{}, std::false_type{});
-        if constexpr (GG < 4) {
-          read_frag(set1, std::integral_constant<int, 2 * GG>{}, K1{}, so);
-          read_frag(set1, std::integral_constant<int, 2 * GG + 1>{}, K1{}, so);
+      constexpr int VMW = cnt(DA, SA1, W) + cnt(DB, SB1, W);
+      static_for<128>([&](auto sc) {
+        constexpr int S = decltype(sc)::value, IDX = S & 63, I = IDX / 8, J = IDX % 8;
+        if constexpr (S < 64) {
+          if constexpr (decltype(zero)::value) mfma_acc0<T>(acc[I][J], set0[8 + J], set0[I]);
+          else mfma_acc<T>(acc[I][J], set0[8 + J], set0[I]);
+        } else {
+          mfma_acc<T>(acc[I][J], set1[8 + J], set1[I]);
         }
-        if constexpr (GG == 5 || GG == 11) {
+        if constexpr (S < 16 && S % 2 == 0)
+          read_frag(set1, std::integral_constant<int, S / 2>{}, K1{}, so);
+        if constexpr (S == B1 || S == B2) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        // (SA / SB == 0: two pieces per group)
-        static_for<8>([&](auto kk) {
-          constexpr int K_ = decltype(kk)::value;
-          constexpr int ga = SA == 0 ? GA + K_ / 2 : GA + SA * K_;
-          constexpr int gb = SB == 0 ? GB + K_ / 2 : GB + SB * K_;
-          if constexpr (ga == GG) dma(K_, ra, soff, slot);
-          if constexpr (gb == GG) dma(8 + K_, rb, soff, slot);
-        });
-        if constexpr (GG >= 6 && GG < 10) {
-          read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
-          read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
-        }
-        if constexpr (GG == WG) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
+        if constexpr (S > B1 && S <= B1 + 15 && (S - B1 - 1) % 2 == 0)
+          read_frag(set1, std::integral_constant<int, 8 + (S - B1 - 1) / 2>{}, K1{}, so);
+        if constexpr (S >= DA && (S - DA) % SA1 == 0 && (S - DA) / SA1 < 8)
+          dma((S - DA) / SA1, ra, soff, slot);
+        if constexpr (S >= DB && (S - DB) % SB1 == 0 && (S - DB) / SB1 < 8)
+          dma(8 + (S - DB) / SB1, rb, soff, slot);
+        if constexpr (S == W) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (GG > WG) {
-          // the 16 fragments of (t+1, k-half 0) spread over groups WG+1 .. 31
-          constexpr int NG = 31 - WG, Q = GG - WG - 1;
-          constexpr int F0 = 16 * Q / NG, F1 = 16 * (Q + 1) / NG;
-          static_for<F1 - F0>([&](auto e) {
-            read_frag(set0, std::integral_constant<int, F0 + decltype(e)::value>{}, K0{}, sn);
+        if constexpr (S > W && S < 127) {
+          // read k at slot W + 1 + floor(k (126 - W) / 16)
+          static_for<16>([&](auto kc) {
+            constexpr int Kr = decltype(kc)::value;
+            if constexpr (W + 1 + (Kr * (126 - W)) / 16 == S)
+              read_frag(set0, std::integral_constant<int, Kr>{}, K0{}, sn);
           });
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1173,35 +1092,6 @@ void launch_nt(NtArgs& p, int kind, int dt, hipStream_t s) {
 }
 
 }  // namespace
-
-void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K,
-                      int mode, hipStream_t s) {
-  NtArgs p{a, b, c, nullptr, nullptr, K, K, N, 0, (int)M, (int)N, (int)K, 0, 0, 0, false,
-           RowMap{}, RowMap{}};
-  p.ntm = (p.M + TM - 1) / TM;
-  p.ntn = (p.N + TN - 1) / TN;
-  p.gm = group_m(p.ntm, p.ntn);
-  const int g = std::min(p.ntm * p.ntn, num_cus());
-  if (mode == 1) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 1>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 2) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 2>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 3) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 3>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 4) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 4>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 5) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 5>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 7) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 7>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 9) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 9>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 10) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 10>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 11) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 11>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 12) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 12>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 13) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 13>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 14) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 14>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 15) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 15>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 16) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 16>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 20) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 20>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 19) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 19>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 18) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 18>), dim3(g), dim3(256), 0, s, p);
-  else if (mode == 17) hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 17>), dim3(g), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((gemm_nt6_k<bf16, EPI_STORE, 0, 0>), dim3(g), dim3(256), 0, s, p);
-}
 
 void gemm_nt_set_variant(int v) {
   v = parse_variant(v);

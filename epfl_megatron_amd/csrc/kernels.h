@@ -244,10 +244,10 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
 void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
                          int64_t K, int mode, hipStream_t s);
 // ---- gemm_nt.hip: C[M,N] = A[M,K] B[N,K]^T (forward / dgrad), GLU epilogues --
-// ablation builds of the persistent NT kernel (bf16, [M,K]x[N,K]^T contiguous): mode 0 full,
-// 1 no DMA in the K-loop, 2 no DMA and no fragment reads
-void gemm_nt_ablation(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K,
-                      int mode, hipStream_t s);
+// Bench-only GEMM experiments (gemm_lab.hip): C = A B^T bf16, variant 0 =
+// production LDS layout, 1 = linear-source padded layout.
+void gemm_lab(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int variant,
+              hipStream_t s);
 void gemm_nt_set_variant(int v);  // 4 or 8 waves per workgroup
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 // Row-group remap of an operand's rows (the chunked TP all-gather / reduce-

@@ -26,14 +26,23 @@
 // epoch e before it reaches e+1), and e+1 writes the other parity.  Epochs are
 // device-side per workgroup, so the launch is hipGraph-capturable.
 //
-// The waits are bounded (2^25 polls, tens of seconds: TP ranks drift apart by
-// host work such as logging between collectives, so a short bound would fire
-// on healthy runs): on timeout the error word is set and the kernel ends
-// instead of hanging the GPU on a dead peer; XgmiAllReduce.check() raises on
-// it, and comm.report() (every training log interval) checks.
+// Ordering (MI355X_MICROARCH "Valid forms", system scope because the peers
+// are other GPUs): every storing wave drains its stores (s_waitcnt vmcnt(0)),
+// the workgroup barrier, then the flag lanes issue a system-scope RELEASE fence,
+// wait for it (asm vmcnt(0): ROCm 7.2 can drop the fence's own wait) and store
+// the flag relaxed; the polling lanes poll relaxed, then issue ONE system-scope
+// ACQUIRE fence and its wait before the barrier that releases the readers.
+//
+// The waits are bounded by wall clock (s_memrealtime, 100 MHz; timeout_ms,
+// default 1 s, EMA_XGMI_TIMEOUT_MS): on timeout the error word is set, the
+// workgroup's output chunk is filled with NaN (never stale partial sums that
+// look valid) and the kernel ends instead of hanging the GPU on a dead peer;
+// XgmiAllReduce.check() raises on the error word, and the training log and
+// every generate call check it.
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -56,6 +65,7 @@ struct XgArgs {
   const char* in;
   char* out;
   int64_t nbytes, cap;
+  uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int rank, world;
 };
 
@@ -68,33 +78,47 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
   const bool valid = off < a.nbytes;
   const unsigned e = a.epoch[b] + 1u;
   const int64_t par = (int64_t)(e & 1u) * a.world * a.cap;
+  __shared__ int timed_out;
+  if (t == 0) timed_out = 0;
   V16<T> v;
   if (valid) {
     v = ld16(reinterpret_cast<const T*>(a.in + off));
     for (int p = 0; p < a.world; ++p)
       st16(reinterpret_cast<T*>(a.data[p] + par + (int64_t)a.rank * a.cap + off), v);
   }
-  // every lane's stores complete and visible system-wide before the workgroup
-  // publishes its chunk
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (t < a.world)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot stores done
+  __syncthreads();                                   // ... and every wave's
+  if (t < a.world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");     // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(a.flags[t] + (int64_t)b * a.world + a.rank, e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-  if (t < a.world) {
     const unsigned* f = a.own_flags + (int64_t)b * a.world + t;
-    int spins = 0;  // (one poll ~1 us: uncached load + sleep)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     // (a peer may already be one epoch ahead: >= in wrap-safe form)
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 25)) {
-        __hip_atomic_store(a.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(a.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");     // system scope, once per lane
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (timed_out) {  // a peer never arrived: poison this chunk of the output
+    if (valid) {
+      V16<T> nan;
+#pragma unroll
+      for (int i = 0; i < V16<T>::N; ++i) nan.v[i] = from_f<T>(__builtin_nanf(""));
+      const int reps = GATHER ? a.world : 1;
+      for (int p = 0; p < reps; ++p) st16(reinterpret_cast<T*>(a.out + (int64_t)p * a.nbytes + off), nan);
+    }
+    if (t == 0) a.epoch[b] = e;
+    return;
+  }
   if (GATHER) {
     if (valid)
       for (int p = 0; p < a.world; ++p)
@@ -186,6 +210,15 @@ void xgmi_open(int64_t id, const void* handles) {
 
 int64_t xgmi_capacity(int64_t id) { return get(id)->cap; }
 
+uint64_t timeout_ticks() {
+  static const uint64_t ticks = [] {
+    const char* e = getenv("EMA_XGMI_TIMEOUT_MS");
+    const long ms = e ? atol(e) : 1000;
+    return (uint64_t)(ms > 0 ? ms : 1000) * 100000ull;  // 100 MHz
+  }();
+  return ticks;
+}
+
 void xgmi_launch(int64_t id, const void* in, void* out, int64_t nbytes, int dt, bool gather,
                  hipStream_t s) {
   XgComm* c = get(id);
@@ -207,6 +240,9 @@ void xgmi_launch(int64_t id, const void* in, void* out, int64_t nbytes, int dt, 
   a.cap = c->cap;
   a.rank = c->rank;
   a.world = c->world;
+  a.timeout_ticks = timeout_ticks();
+  if ((uintptr_t)in % 16 || (uintptr_t)out % 16)
+    throw std::runtime_error("xgmi: input and output must be 16-B aligned (parallel/xgmi.py stages)");
   const unsigned grid = (unsigned)((nbytes + XG_CHUNK - 1) / XG_CHUNK);
   if (gather) {
     EMA_DISPATCH_FLOAT(dt, T, {

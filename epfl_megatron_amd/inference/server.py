@@ -7,8 +7,10 @@
 ``beam_width``, ``stop_token``, ``length_penalty``) answering
 ``{"text", "segments", "logprobs"}`` or ``{"text", "segments", "scores"}``.
 
-Flask is not part of this image, so the app is FastAPI/uvicorn; ``GET /``
-serves the small web UI in ``static/index.html`` (reference ``megatron/static``).  Validation
+The app is FastAPI/uvicorn (the reference used Flask-RESTful; FastAPI gives
+request validation and an ASGI server with the same ``PUT /api`` contract);
+``GET /`` serves the small web UI in ``static/index.html`` (reference
+``megatron/static``).  Validation
 lives in :func:`parse_request` (pure, unit-tested); invalid requests get HTTP
 400 with the reference's message (the reference answered some of them with
 200).  Rank 0 serves; before each request it broadcasts a command code

@@ -64,7 +64,9 @@ def rccl_watchdog_env(timeout_minutes, environ=None):
         "TORCH_NCCL_ENABLE_MONITORING": "1",
         "TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC": str(max(60, int(timeout_minutes * 60))),
         "TORCH_NCCL_DUMP_ON_TIMEOUT": "1",
-        "TORCH_NCCL_TRACE_BUFFER_SIZE": "2000",
+        # flight-recorder depth (the TORCH_NCCL_TRACE_BUFFER_SIZE spelling is
+        # deprecated in torch 2.10 and warns on every run)
+        "TORCH_FR_BUFFER_SIZE": "2000",
     }
     for k, v in want.items():
         environ.setdefault(k, v)

@@ -266,6 +266,33 @@ def _kernel_ok(a, w):
     return a.is_cuda and ext().gemm_nt_supported(a, w)
 
 
+# GPU products that could not take the hand-written NT kernel (dtype / shape /
+# alignment outside csrc/gemm_nt.hip's contract) and ran as torch math
+# instead.  Counted per (op, reason), warned once each, reported by
+# training_log; EMA_STRICT_KERNELS=1 turns them into errors.
+FALLBACKS = {}
+_STRICT = os.environ.get("EMA_STRICT_KERNELS", "0") == "1"
+
+
+def _note_fallback(op, a, w):
+    if not a.is_cuda:
+        return  # CPU / gloo: torch math is the implementation
+    key = (op, str(a.dtype), tuple(w.shape))
+    if _STRICT:
+        raise RuntimeError(f"{op}: no HIP kernel for {a.dtype} {tuple(a.shape)} x "
+                           f"{tuple(w.shape)} (EMA_STRICT_KERNELS=1)")
+    if key not in FALLBACKS:
+        warnings.warn(f"{op}: {a.dtype} {tuple(a.shape)} x {tuple(w.shape)} is outside the "
+                      "NT GEMM kernel's contract; running torch math (counted in "
+                      "layers.FALLBACKS)", stacklevel=3)
+    FALLBACKS[key] = FALLBACKS.get(key, 0) + 1
+
+
+def fallback_report():
+    """``{"op dtype shape": count}`` of GPU GEMMs that ran as torch math."""
+    return {f"{k[0]} {k[1]} {list(k[2])}": v for k, v in FALLBACKS.items()}
+
+
 def gemm(a, w, out=None, a_map=None, c_map=None, m=None):
     """out[c_map(q)] = a[a_map(q)] @ w^T for logical rows q < m (default: all
     rows of ``a``).  Maps: (rows, stride, offset) — see csrc/kernels.h RowMap."""
@@ -277,6 +304,7 @@ def gemm(a, w, out=None, a_map=None, c_map=None, m=None):
         return torch.matmul(a, w.t(), out=out)
     if _kernel_ok(a, w) and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0)):
         return ext().gemm_nt(a, w, out, list(a_map or []), list(c_map or []), m)
+    _note_fallback("gemm", a, w)
     src = _rows_view(a, a_map, m).reshape(m, a.shape[-1])
     res = src @ w.t()
     if out is None:
@@ -293,6 +321,7 @@ def gemm_glu(a, w1, kind, pre=None, y=None, c_map=None):
     """(pre, y) = (a @ w1^T, x1 * act(x2)) with x1 / x2 the up / gate halves."""
     if _kernel_ok(a, w1):
         return ext().gemm_nt_glu(a, w1, kind, pre, y, list(c_map or []))
+    _note_fallback("gemm_glu", a, w1)
     p = a @ w1.t()
     f = w1.shape[0] // 2
     yy = p[:, :f] * _act(kind, p[:, f:])
@@ -308,6 +337,7 @@ def gemm_dglu(g, w2t, pre, kind, out=None):
     (written into ``out`` [M, 2F] when given)."""
     if _kernel_ok(g, w2t):
         return ext().gemm_nt_dglu(g, w2t, pre, kind, out)
+    _note_fallback("gemm_dglu", g, w2t)
     da = g @ w2t.t()
     f = w2t.shape[0]
     x1, x2 = pre[:, :f], pre[:, f:]

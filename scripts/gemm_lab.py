@@ -1,9 +1,9 @@
-"""Where the persistent NT GEMM (csrc/gemm_nt.hip variant 6) loses time:
-interleaved timing (one process, CDNA guide rule 24) of the full kernel, the
-kernel without its K-loop DMA, the kernel with neither DMA nor fragment reads
-(MFMA + barriers + epilogue), and hipBLASLt, on uniform-random bf16 operands.
+"""A/B of bench-only GEMM builds (csrc/gemm_lab.hip) against the production
+persistent NT kernel and hipBLASLt: interleaved timing in one process (CDNA
+guide rule 24), uniform-random bf16 operands, median over rounds.  Variant 1
+is also checked against hipBLASLt's output.
 
-    python scripts/gemm_ablation.py [M N K ...]
+    python scripts/gemm_lab.py [M N K ...]
 """
 import os
 import statistics
@@ -28,20 +28,29 @@ def _t(fn, iters=10):
 
 def main():
     C = ext()
+    C.gemm_nt_set_variant(6)  # production = the persistent kernel
     args = [int(v) for v in sys.argv[1:]]
     shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or \
-        [(16384, 4096, 4096), (16384, 4096, 11008), (16384, 11008, 4096)]
+        [(16384, 4096, 4096), (16384, 4096, 11008), (16384, 11008, 4096), (16384, 12288, 4096)]
+    variants = [int(v) for v in os.environ.get("LAB_VARIANTS", "0,1").split(",")]
     for M, N, K in shapes:
         a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ref = torch.matmul(a, b.t())
+        for v in variants:
+            c.zero_()
+            C.gemm_lab(a, b, c, v)
+            err = ((c.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+            assert err < 2e-2, f"variant {v} wrong: rel err {err}"
         fl = 2.0 * M * N * K
-        modes = ((0, "production"), (1, "no_dma"), (2, "mfma_only"), (14, "burst(r4e)"))
-        r = {k: [] for _, k in modes}
+        r = {f"lab{v}": [] for v in variants}
+        r["prod"] = []
         r["hipblaslt"] = []
         for _ in range(5):
-            for mode, k in modes:
-                r[k].append(fl / _t(lambda: C.gemm_nt_ablation(a, b, c, mode)) / 1e12)
+            for v in variants:
+                r[f"lab{v}"].append(fl / _t(lambda: C.gemm_lab(a, b, c, v)) / 1e12)
+            r["prod"].append(fl / _t(lambda: C.gemm_nt(a, b, c)) / 1e12)
             r["hipblaslt"].append(fl / _t(lambda: torch.matmul(a, b.t(), out=c)) / 1e12)
         print(f"M={M} N={N} K={K}: " + "  ".join(
             f"{k} {statistics.median(v):7.1f}" for k, v in r.items()) + " TF/s", flush=True)

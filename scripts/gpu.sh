@@ -1,0 +1,86 @@
+#!/bin/bash
+# One parametrised GPU runner for gpurun (replaces the per-experiment
+# scripts/gpu_r*.sh launchers):
+#
+#   bash scripts/gpu.sh TAG STEP [STEP ...]
+#
+# Every step runs under its own time limit, logs to gpurun_out/TAG_STEP.log,
+# and the first failing step ends the call (no GPU work after a fault, an
+# abort or a time limit).  Steps:
+#   tests      pytest -m gpu (one process)
+#   quick      pytest -m gpu on the kernel / GEMM numerics files only
+#   smoke      __graft_entry__.smoke()
+#   bench      bench.py --steps 8 --warmup 2 (the headline config)
+#   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
+#   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
+#   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
+#   wgrad      scripts/wgrad_bench.py
+#   fa         scripts/fa_bench.py
+#   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
+#   px70       bench.py --proxy llama70b-tp8
+#   pmc_lab    rocprofv3 --pmc passes over scripts/gemm_lab.py (one pass per run)
+# Extra bench.py arguments: BENCH_ARGS="..." in the environment.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+TAG=$1
+shift
+[ -n "$TAG" ] || { echo "usage: gpu.sh TAG STEP..."; exit 2; }
+
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2
+  shift 2
+  local log="gpurun_out/${TAG}_${name}.log"
+  echo "== ${name} (limit ${secs}s)"
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  local rc=$?
+  tail -n 4 "$log" | cut -c1-600
+  if [ $rc -ne 0 ]; then
+    echo "step ${name} failed rc=${rc}"
+    tail -n 40 "$log"
+    exit 1
+  fi
+}
+
+prof() {  # prof NAME SECONDS CMD...  (rocprofv3 kernel trace + stats)
+  local name=$1 secs=$2
+  shift 2
+  export TMPDIR=/tmp
+  run "$name" "$secs" rocprofv3 --kernel-trace --stats --output-format csv \
+    -d "gpurun_out/${TAG}_${name}" -o prof -- "$@"
+  find "gpurun_out/${TAG}_${name}" -name "*kernel_stats.csv" | head -3
+}
+
+for step in "$@"; do
+  case $step in
+    tests) run tests 1000 python -u -m pytest -x -q --timeout 280 --timeout-method thread \
+             -p no:cacheprovider tests -m gpu ;;
+    quick) run quick 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+             -p no:cacheprovider tests/test_kernels_gpu.py tests/test_gemm_gpu.py -m gpu ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 500 python -u bench.py --steps 8 --warmup 2 $BENCH_ARGS ;;
+    prof) prof prof 600 python3 -u bench.py --steps 2 --warmup 1 $BENCH_ARGS ;;
+    lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
+    gemm) run gemm 400 python -u scripts/gemm_nt_bench.py ;;
+    wgrad) run wgrad 400 python -u scripts/wgrad_bench.py ;;
+    fa) run fa 400 python -u scripts/fa_bench.py ;;
+    px7) run px7 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
+    px70) run px70 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;
+    pmc_lab)
+      export TMPDIR=/tmp
+      i=0
+      for ctr in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+                 "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" \
+                 "TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE"; do
+        i=$((i + 1))
+        run "pmc${i}" 120 rocprofv3 --pmc $ctr --output-format csv -d "gpurun_out/${TAG}_pmc${i}" -o pmc -- \
+          python3 -u scripts/gemm_lab.py $LAB_SHAPES
+      done
+      python scripts/pmc_table.py gpurun_out/${TAG}_pmc* > "gpurun_out/${TAG}_pmc_table.txt" 2>&1
+      cat "gpurun_out/${TAG}_pmc_table.txt" | cut -c1-400 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done"

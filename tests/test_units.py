@@ -3,6 +3,7 @@ tensor_parallel/test_{mappings,cross_entropy,random,data,tensor_parallel_utils})
 plus scheduler / grad scaler / microbatch / checkpoint-resume coverage.
 Multi-rank cases run on gloo (the reference needed 8 GPUs for these)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -325,6 +326,42 @@ def test_validate_args_derivations():
     assert not args.sequence_parallel
 
 
+def test_reference_flag_spellings():
+    """Reference spellings parse with the reference semantics:
+    --barrier_with_L1_time is store_false (megatron/arguments.py:492), the
+    descriptive alias sets the same dest, and --use_ring_exchange_p2p is
+    accepted but warns that it is ignored."""
+    import warnings
+    from epfl_megatron_amd.config.arguments import parse_args, validate_args
+    base = ["--num_layers", "2", "--hidden_size", "64", "--num_attention_heads", "8",
+            "--seq_length", "32", "--max_position_embeddings", "32", "--micro_batch_size", "1"]
+    assert parse_args(None, base).barrier_with_L1_time is True
+    assert parse_args(None, base + ["--barrier_with_L1_time"]).barrier_with_L1_time is False
+    assert parse_args(None, base + ["--no_barrier_with_level_1_timing"]).barrier_with_L1_time is False
+    a = parse_args(None, base + ["--use_ring_exchange_p2p"])
+    a.rank, a.world_size = 0, 1
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        validate_args(a, {})
+    assert any("use_ring_exchange_p2p" in str(x.message) for x in w)
+
+
+def test_every_reference_flag_parses():
+    """Every flag the reference's argument parser defines is accepted here
+    (Appendix A: reference launch scripts run unchanged).  Parity unpinned
+    when the reference tree is absent."""
+    import re
+    ref = "/root/reference/megatron/arguments.py"
+    if not os.path.exists(ref):
+        pytest.skip("reference tree not present")
+    from epfl_megatron_amd.config.arguments import build_base_parser
+    names = set(re.findall(r"add_argument\(\s*['\"](--[A-Za-z0-9_\-]+)['\"]", open(ref).read()))
+    assert len(names) > 150
+    known = set(build_base_parser()._option_string_actions)
+    missing = sorted(n for n in names if n not in known)
+    assert not missing, missing
+
+
 def test_context_parallel_refuses_attention_dropout():
     """Ring attention has no attention dropout, so CP > 1 with a non-zero
     --attention_dropout on the non-flash path is refused."""
@@ -435,6 +472,8 @@ def test_rccl_watchdog_env():
     assert env["TORCH_NCCL_ENABLE_MONITORING"] == "1"
     assert env["TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC"] == "600"
     assert env["TORCH_NCCL_DUMP_ON_TIMEOUT"] == "1"
+    assert env["TORCH_FR_BUFFER_SIZE"] == "2000"
+    assert "TORCH_NCCL_TRACE_BUFFER_SIZE" not in env  # deprecated spelling
 
 
 def test_decode_pack_layout():
