@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from . import ckpt_pickle, global_vars
+from .ops import decode_pack
 from .parallel import state
 from .parallel.tensor.random import get_cuda_rng_tracker
 from .models import enums as _enums
@@ -433,6 +434,7 @@ def load_checkpoint(model, optimizer, opt_param_scheduler, load_arg="load", stri
             state.set_virtual_pipeline_model_parallel_rank(i)
             m.load_state_dict(model_sd[f"model{i}"], strict=strict)
     fix_query_key_value_ordering(model[0], get_checkpoint_version())
+    decode_pack.bump_weight_generation()  # weights replaced: derived copies are stale
     if optimizer is not None:
         optimizer.reload_model_params()
     if not release and not args.finetune and not args.no_load_optim:

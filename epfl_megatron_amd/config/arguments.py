@@ -245,6 +245,11 @@ FLAG_TABLE = {
                    "many KiB per rank (contiguous, 16-B sized) through the one-shot xGMI "
                    "peer-memory kernel (parallel/xgmi.py) instead of RCCL; 0 = off.  For the "
                    "latency-bound [b, h] all-reduces and logits all-gathers of TP decode"),
+        _flag("--tp_xgmi_allgather_kb", type=int, default=None,
+              help="per-rank cap (KiB) of the tensor-parallel all-gathers routed through the "
+                   "one-shot xGMI kernel (default: --tp_xgmi_allreduce_kb).  Sized for the "
+                   "sequence-parallel [s/tp, b, h] pieces (multi-MiB) it lets the all-gather "
+                   "take the W-1 links at once instead of an RCCL ring"),
         _flag("--no_overlap_grad_reduce", action="store_false", dest="overlap_grad_reduce"),
         _flag("--no_overlap_param_gather", action="store_false", dest="overlap_param_gather",
               help="dist-opt: all-gather parameters synchronously at step end instead of "
@@ -587,10 +592,11 @@ def _derive_recompute_and_parallel_features(args):
         _require(args.attention_dropout == 0 or args.use_flash_attn,
                  "context parallelism applies no attention dropout: set --attention_dropout 0 "
                  "(or --use_flash_attn, which has none either)")
-    xg = getattr(args, "tp_xgmi_allreduce_kb", 0) or 0
-    _require(xg >= 0 and xg % 4 == 0 and xg <= 65536,
-             "--tp_xgmi_allreduce_kb must be a multiple of 4 in [0, 65536] "
-             "(the one-shot kernel moves 4 KiB per workgroup)")
+    for flag in ("tp_xgmi_allreduce_kb", "tp_xgmi_allgather_kb"):
+        xg = getattr(args, flag, 0) or 0
+        _require(xg >= 0 and xg % 4 == 0 and xg <= 65536,
+                 f"--{flag} must be a multiple of 4 in [0, 65536] "
+                 "(the one-shot kernel moves 4 KiB per workgroup)")
     # Reference defect D17: the GQA view silently breaks when KV heads do not
     # split evenly over TP ranks; we check it explicitly.
     if args.num_attention_heads_kv % (sim_tp or args.tensor_model_parallel_size) != 0:

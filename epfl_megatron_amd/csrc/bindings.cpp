@@ -748,7 +748,7 @@ at::Tensor skinny_norm_glu(const at::Tensor& x, const at::Tensor& w1,
   const int64_t F = w1.size(0) / 2;
   TORCH_CHECK(w1.size(0) == 2 * F && F % 8 == 0 &&
               ema::skinny_gemm_supported(p.M, 2 * F, p.K), "skinny glu: unsupported shape");
-  TORCH_CHECK(!packed || packed_tail == ema::skinny_glu_half_tail(F, p.K, norm_w.has_value()),
+  TORCH_CHECK(!packed || packed_tail == ema::skinny_glu_half_tail(F, p.K, norm_w.has_value(), p.M),
               "skinny glu: weight packed for another half-unit tail (skinny_glu_half_tail)");
   auto y = at::empty({p.M, F}, x.options());
   p.N = (int)F;
@@ -1282,7 +1282,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("res"), py::arg("packed") = false);
   m.def("skinny_norm_glu", &skinny_norm_glu, py::arg("x"), py::arg("w1"), py::arg("norm_w"),
         py::arg("eps"), py::arg("kind"), py::arg("packed") = false, py::arg("packed_tail") = 0);
-  m.def("skinny_glu_half_tail", &ema::skinny_glu_half_tail);
+  m.def("skinny_glu_half_tail", &ema::skinny_glu_half_tail, py::arg("F"), py::arg("K"),
+        py::arg("norm"), py::arg("M") = 1);
   m.def("skinny_qkv_rope_cache", &skinny_qkv_rope_cache, py::arg("x"), py::arg("w"),
         py::arg("norm_w"), py::arg("eps"), py::arg("ng"), py::arg("r"), py::arg("hd"),
         py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("kcache"), py::arg("vcache"),

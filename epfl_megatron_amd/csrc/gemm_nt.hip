@@ -57,6 +57,7 @@
 
 #include "act_math.h"
 #include "fa_common.h"
+#include "gemm_plan.h"
 
 namespace ema {
 namespace {
@@ -932,21 +933,9 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
       const uint32_t soff = (uint32_t)((here ? t + 2 : t + 2 - nt) * BK2 * (int)sizeof(T));
-      // One-MFMA slot plan (slot s = MFMA index, at most ~1 other instruction
-      // after each MFMA, the issue pattern of the vendor 256x256 kernel; +3-6 %
-      // over groups of four MFMAs, profiles/r4k_gemm_ablation.txt):
-      //   A-k-half-1 reads at 2k (k < 8), barrier 1 after slot B1, the B k-half-1
-      //   reads from B1 + 1 every 2, barrier 2 after B2, A DMA piece k at DA + SA1 k,
-      //   B piece k at DB + SB1 k (spread: the per-CU L2 -> LDS fill path stalls
-      //   on bursts, profiles/r4f_gemm_ablation.txt), the step-t+1 wait after W,
-      //   then the 16 reads of (t+1, k-half 0) spread to slot 126.
-      constexpr int B1 = 17, B2 = 35, DA = B1 + 2, SA1 = 4, DB = B2 + 2, SB1 = 8, W = 95;
-      auto cnt = [](int d, int st, int w) constexpr {
-        int n = 0;
-        for (int k = 0; k < 8; ++k) n += d + st * k <= w;
-        return n;
-      };
-      constexpr int VMW = cnt(DA, SA1, W) + cnt(DB, SB1, W);
+      // One-MFMA slot plan (kNtPlan: events after MFMA index S; +1-5 % over
+      // the round-4 plan, profiles/r5e_gemm_lab.txt)
+      constexpr int VMW = nt_plan_vmw();
       static_for<128>([&](auto sc) {
         constexpr int S = decltype(sc)::value, IDX = S & 63, I = IDX / 8, J = IDX % 8;
         if constexpr (S < 64) {
@@ -955,31 +944,21 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
         } else {
           mfma_acc<T>(acc[I][J], set1[8 + J], set1[I]);
         }
-        if constexpr (S < 16 && S % 2 == 0)
-          read_frag(set1, std::integral_constant<int, S / 2>{}, K1{}, so);
-        if constexpr (S == B1 || S == B2) {
+        static_for<16>([&](auto ec) {
+          constexpr int E = decltype(ec)::value;
+          if constexpr (kNtPlan.rd1[E] == S) read_frag(set1, std::integral_constant<int, E>{}, K1{}, so);
+          if constexpr (kNtPlan.dma[E] == S) dma(E, E < 8 ? ra : rb, soff, slot);
+          if constexpr (kNtPlan.rd0[E] == S) read_frag(set0, std::integral_constant<int, E>{}, K0{}, sn);
+        });
+        if constexpr (S == kNtPlan.b1 || S == kNtPlan.b2) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (S > B1 && S <= B1 + 15 && (S - B1 - 1) % 2 == 0)
-          read_frag(set1, std::integral_constant<int, 8 + (S - B1 - 1) / 2>{}, K1{}, so);
-        if constexpr (S >= DA && (S - DA) % SA1 == 0 && (S - DA) / SA1 < 8)
-          dma((S - DA) / SA1, ra, soff, slot);
-        if constexpr (S >= DB && (S - DB) % SB1 == 0 && (S - DB) / SB1 < 8)
-          dma(8 + (S - DB) / SB1, rb, soff, slot);
-        if constexpr (S == W) {
+        if constexpr (S == kNtPlan.w) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
-        }
-        if constexpr (S > W && S < 127) {
-          // read k at slot W + 1 + floor(k (126 - W) / 16)
-          static_for<16>([&](auto kc) {
-            constexpr int Kr = decltype(kc)::value;
-            if constexpr (W + 1 + (Kr * (126 - W)) / 16 == S)
-              read_frag(set0, std::integral_constant<int, Kr>{}, K0{}, sn);
-          });
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1020,15 +999,16 @@ int group_m(int ntm, int ntn) {
     default: { constexpr int A_ = 3; __VA_ARGS__; break; }    \
   }
 
-// Kernel variant per epilogue: 5 (one-shot early-refill 4-wave), 6 (persistent
-// 4-wave, register epilogue), 4 (one-shot, one refill point), 8 (8-wave
-// ping-pong).  Defaults from interleaved same-box A/B on the 7B shapes
-// (profiles/r4g_gemm_nt_bench.txt): fc2 dgrad + dGLU on 6 (1.07x hipBLASLt +
-// glu kernel vs 1.05x on 5), fc1 + GLU on 5 (1.01x vs 0.97x), plain products
-// on 5 (they run on hipBLASLt in-model unless a row map needs this kernel).
+// Kernel variant per epilogue: 6 (persistent 4-wave, register epilogue; row
+// maps fall back to 5), 5 (one-shot early-refill 4-wave), 4 (one-shot, one
+// refill point), 8 (8-wave ping-pong).  Defaults from interleaved same-box
+// A/B on the 7B shapes (profiles/r5g_gemm_nt_bench.txt): 6 everywhere (fc1 +
+// GLU 1.04x hipBLASLt + glu kernel vs 1.02x on 5; fc2 dgrad + dGLU 1.13x vs
+// 1.05x; plain products 0.93-0.99x hipBLASLt, so those stay on hipBLASLt
+// in-model unless a row map needs this kernel).
 // EMA_GEMM_NT=<v> or gemm_nt_set_variant(v) forces one variant everywhere
 // (A/B in one process); gemm_nt_set_variant(0) restores the defaults.
-int g_var[3] = {5, 5, 6};  // [EPI_STORE, EPI_GLU, EPI_DGLU]
+int g_var[3] = {6, 6, 6};  // [EPI_STORE, EPI_GLU, EPI_DGLU]
 int parse_variant(int v) { return (v == 4 || v == 5 || v == 6 || v == 8) ? v : 0; }
 const int g_env_variant = [] {
   const char* e = getenv("EMA_GEMM_NT");
@@ -1098,7 +1078,7 @@ void gemm_nt_set_variant(int v) {
   if (v) {
     g_var[0] = g_var[1] = g_var[2] = v;
   } else {
-    g_var[0] = 5; g_var[1] = 5; g_var[2] = 6;
+    g_var[0] = 6; g_var[1] = 6; g_var[2] = 6;
   }
 }
 

@@ -54,6 +54,7 @@
 #include <cstdlib>
 
 #include "fa_common.h"
+#include "gemm_plan.h"
 
 namespace ema {
 namespace {
@@ -581,14 +582,6 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
-  auto mfma4 = [&](X8 (&cur)[16], auto gq, auto zero) {
-    constexpr int GG = decltype(gq)::value;
-    static_for<4>([&](auto q) {
-      constexpr int IDX = 4 * GG + decltype(q)::value, I = IDX / 8, J = IDX % 8;
-      if constexpr (decltype(zero)::value) wmfma0<T>(acc[I][J], cur[8 + J], cur[I]);
-      else wmfma<T>(acc[I][J], cur[8 + J], cur[I]);
-    });
-  };
 
   Rsrc ra_c, rb_c, ra_n, rb_n;
   make_rsrc(0, ra_c, rb_c);
@@ -609,35 +602,32 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
       const int s2 = here ? t + 2 : t + 2 - nt;
-      static_for<32>([&](auto gq) {
-        constexpr int GG = decltype(gq)::value;
-        if constexpr (GG < 16) mfma4(set0, std::integral_constant<int, GG>{}, zero);
-        else mfma4(set1, std::integral_constant<int, GG - 16>{}, std::false_type{});
-        if constexpr (GG < 4) {
-          read_frag(set1, std::integral_constant<int, 2 * GG>{}, K1{}, so);
-          read_frag(set1, std::integral_constant<int, 2 * GG + 1>{}, K1{}, so);
+      // the shared slot plan (gemm_plan.h) with A = dY, B = X: dY's pieces of
+      // step t+2 after barrier 1, X's after barrier 2, 13 before the wait
+      constexpr int VMW = nt_plan_vmw();
+      static_for<128>([&](auto sc) {
+        constexpr int S = decltype(sc)::value, IDX = S & 63, I = IDX / 8, J = IDX % 8;
+        if constexpr (S < 64) {
+          if constexpr (decltype(zero)::value) wmfma0<T>(acc[I][J], set0[8 + J], set0[I]);
+          else wmfma<T>(acc[I][J], set0[8 + J], set0[I]);
+        } else {
+          wmfma<T>(acc[I][J], set1[8 + J], set1[I]);
         }
-        if constexpr (GG == 5 || GG == 11) {
+        static_for<16>([&](auto ec) {
+          constexpr int E = decltype(ec)::value;
+          if constexpr (kNtPlan.rd1[E] == S) read_frag(set1, std::integral_constant<int, E>{}, K1{}, so);
+          if constexpr (kNtPlan.dma[E] == S) dmaq(E, ra, rb, s2, slot);
+          if constexpr (kNtPlan.rd0[E] == S) read_frag(set0, std::integral_constant<int, E>{}, K0{}, sn);
+        });
+        if constexpr (S == kNtPlan.b1 || S == kNtPlan.b2) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        // DMA pieces spread over the K-step (dY at groups 6, 8, .., 20; X at
-        // 13, 15, .., 27): the per-CU fill path stalls on bursts (gemm_nt.hip)
-        if constexpr (GG >= 6 && GG <= 20 && (GG - 6) % 2 == 0) dmaq((GG - 6) / 2, ra, rb, s2, slot);
-        if constexpr (GG >= 6 && GG < 10) {
-          read_frag(set1, std::integral_constant<int, 8 + 2 * (GG - 6)>{}, K1{}, so);
-          read_frag(set1, std::integral_constant<int, 9 + 2 * (GG - 6)>{}, K1{}, so);
-        }
-        if constexpr (GG >= 13 && GG <= 27 && (GG - 13) % 2 == 0) dmaq(8 + (GG - 13) / 2, ra, rb, s2, slot);
-        if constexpr (GG == 23) {
-          asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // 8 dY + 6 X pieces of step t+2 may fly
+        if constexpr (S == kNtPlan.w) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
-        }
-        if constexpr (GG >= 24) {
-          read_frag(set0, std::integral_constant<int, 2 * (GG - 24)>{}, K0{}, sn);
-          read_frag(set0, std::integral_constant<int, 2 * (GG - 24) + 1>{}, K0{}, sn);
         }
         __builtin_amdgcn_sched_barrier(0);
       });

@@ -300,7 +300,7 @@ struct SkinnyArgs {
   int packed;           // 1: w is in the decode-packed layout (skinny_pack, K % 256 == 0)
 };
 void skinny_gemm_ex(const SkinnyArgs& p, int epi, int dt, hipStream_t s);
-int skinny_glu_half_tail(int64_t F, int64_t K, bool norm);
+int skinny_glu_half_tail(int64_t F, int64_t K, bool norm, int64_t M);
 
 // ---- transpose.hip -------------------------------------------------------------------------------
 // dst[cols, rows] = src[rows, cols]^T for 16-bit elements; rows, cols multiples of 64.

@@ -694,16 +694,20 @@ void skinny_gemm_ex(const SkinnyArgs& p0, int epi, int dt, hipStream_t s) {
 }
 
 // GLU blocks of 8 features (F / 8) the persistent kernel runs as half units
-// in its last round (0: none / not the persistent form).  The decode-packed
-// GLU weight stores exactly these tail blocks in the half-unit layout.
-int skinny_glu_half_tail(int64_t F, int64_t K, bool norm) {
+// in its last round (0: none / not the persistent form) for an M-row call
+// with (norm) or without the RMSNorm prologue.  The decode-packed GLU weight
+// stores exactly these tail blocks in the half-unit layout.  The condition
+// mirrors skinny_gemm_ex + dispatch: K = 4096 is always persistent; K = 8192
+// only un-normed with <= 16 rows (17-32 rows and the normed forms run the
+// one-block-per-workgroup kernel, which reads no half units).
+int skinny_glu_half_tail(int64_t F, int64_t K, bool norm, int64_t M) {
   static const bool persist = [] {
     const char* e = getenv("EMA_SKINNY_PERSIST");
     return !(e && e[0] == '0');
   }();
   if (K % 256 != 0 || F % 8 != 0) return 0;
   const int64_t steps = K / 256;
-  if (!persist || !(steps == 16 || (steps == 32 && !norm))) return 0;
+  if (!persist || !(steps == 16 || (steps == 32 && !norm && M <= 16))) return 0;
   const int64_t nblocks = F / 8, G = nblocks < num_cus() ? nblocks : num_cus();
   const int64_t nrem = nblocks % G;
   return nrem > 0 && 2 * nrem <= G ? (int)nrem : 0;

@@ -6,7 +6,7 @@ same generation loop.
 """
 import torch
 
-from ..parallel import state
+from ..parallel import comm, state
 from .communication import broadcast_float_list, device
 from .generation import (beam_search_and_return_on_first_stage,
                          generate_tokens_probs_and_return_on_first_stage,
@@ -59,14 +59,17 @@ def generate(model, prompts=None, tokens_to_generate=0, return_output_log_probs=
     toks, lens = tokenize_prompts(prompts=prompts, tokens_to_generate=tokens_to_generate,
                                   add_BOS=bool(add_BOS))
     if tokens_to_generate == 0:
-        return score_and_return_on_first_stage(model, toks, lens)
-    return generate_tokens_probs_and_return_on_first_stage(
-        model, toks, lens, return_output_log_probs=bool(return_output_log_probs),
-        top_k=top_k_sampling, top_p=top_p_sampling, top_p_decay=top_p_decay,
-        top_p_bound=top_p_bound, temperature=temperature,
-        use_eod_token_for_early_termination=bool(use_eod),
-        stop_on_double_eol=bool(stop_on_double_eol), stop_on_eol=bool(stop_on_eol),
-        prevent_newline_after_colon=bool(prevent_newline_after_colon))
+        out = score_and_return_on_first_stage(model, toks, lens)
+    else:
+        out = generate_tokens_probs_and_return_on_first_stage(
+            model, toks, lens, return_output_log_probs=bool(return_output_log_probs),
+            top_k=top_k_sampling, top_p=top_p_sampling, top_p_decay=top_p_decay,
+            top_p_bound=top_p_bound, temperature=temperature,
+            use_eod_token_for_early_termination=bool(use_eod),
+            stop_on_double_eol=bool(stop_on_double_eol), stop_on_eol=bool(stop_on_eol),
+            prevent_newline_after_colon=bool(prevent_newline_after_colon))
+    comm.check_xgmi()  # a one-shot TP collective that timed out poisoned the tokens: raise
+    return out
 
 
 def beam_search_and_post_process(model, prompts=None, tokens_to_generate=0, beam_size=0,
@@ -94,6 +97,8 @@ def beam_search(model, prompts=None, tokens_to_generate=0, beam_size=0, add_BOS=
     length_penalty, prevent_newline_after_colon = vals[5], bool(vals[6])
     toks, lens = tokenize_prompts(prompts=prompts, tokens_to_generate=tokens_to_generate,
                                   add_BOS=add_BOS)
-    return beam_search_and_return_on_first_stage(
+    out = beam_search_and_return_on_first_stage(
         model, toks, lens, beam_size, stop_token=stop_token, num_return_gen=num_return_gen,
         length_penalty=length_penalty, prevent_newline_after_colon=prevent_newline_after_colon)
+    comm.check_xgmi()
+    return out

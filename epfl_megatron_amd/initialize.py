@@ -117,11 +117,16 @@ def _initialize_distributed(args):
         state.set_tensor_model_parallel_world_size(sim_tp)
         state.set_tensor_model_parallel_rank(0)
         comm.set_loopback(state.get_tensor_model_parallel_group(), sim_tp)
-    xg_kb = getattr(args, "tp_xgmi_allreduce_kb", 0)
-    if (xg_kb and state.get_tensor_model_parallel_world_size() > 1 and not (sim_tp and sim_tp > 1)
-            and torch.cuda.is_available()):
+    xg_kb = getattr(args, "tp_xgmi_allreduce_kb", 0) or 0
+    ag_kb = getattr(args, "tp_xgmi_allgather_kb", None)
+    ag_kb = xg_kb if ag_kb is None else ag_kb
+    if ((xg_kb or ag_kb) and state.get_tensor_model_parallel_world_size() > 1
+            and not (sim_tp and sim_tp > 1) and torch.cuda.is_available()):
+        # (on gloo / CPU the flags are accepted and nothing is registered:
+        # the one-shot kernel needs GPU peer memory)
         from .parallel import comm
-        comm.enable_xgmi_allreduce(state.get_tensor_model_parallel_group(), xg_kb * 1024)
+        comm.enable_xgmi_allreduce(state.get_tensor_model_parallel_group(), xg_kb * 1024,
+                                   ag_kb * 1024)
     if args.world_size > 1 and getattr(args, "comm_selfcheck", True):
         from .parallel.selfcheck import collective_selfcheck
         collective_selfcheck()

@@ -520,13 +520,14 @@ class ParallelTransformerLayer(MegatronModule):
         # weights in the decode-packed layout when the shape allows (ops/decode_pack.py)
         wq, wo = sa.query_key_value.weight, sa.dense.weight
         w1, w2 = mlp.dense_h_to_4h.weight, mlp.dense_4h_to_h.weight
-        pq, po = decode_pack.packed(wq), decode_pack.packed(wo)
-        tail = C.skinny_glu_half_tail(w1.shape[0] // 2, w1.shape[1], True)
-        p1, p2 = decode_pack.packed(w1, glu=True, half_tail=tail), decode_pack.packed(w2)
         # 17-32 rows: the norm runs as its own kernel and the projections take
         # the un-normed two-row-block forms (the normed ones spill their 2 x 16
         # X fragments: profiles/r4ai_skinny_mb.txt)
         sep = b > 16
+        pq, po = decode_pack.packed(wq), decode_pack.packed(wo)
+        # the half-unit tail of the form that will run (normed for <= 16 rows)
+        tail = C.skinny_glu_half_tail(w1.shape[0] // 2, w1.shape[1], not sep, b)
+        p1, p2 = decode_pack.packed(w1, glu=True, half_tail=tail), decode_pack.packed(w2)
         xq = rms_norm(x, ln1.weight, ln1.eps) if sep else x
         q = C.skinny_qkv_rope_cache(xq, wq if pq is None else pq, None if sep else ln1.weight,
                                     ln1.eps, ng, r, hd,

@@ -22,10 +22,14 @@ units ``[unit, wave, s, q, pr, e]`` (512 B per k-step) with ``pr`` = the 4 up
 then the 4 gate rows of features ``8 b + 4 h .. + 3``; MFMA rows r and r + 4
 of a half unit read the same bytes.
 
-The packed copy lives next to the parameter (``_ema_decode_packed``) and is
-rebuilt when the parameter's storage or in-place version changes, i.e. after
-an optimizer step or a checkpoint load; 288 GB of HBM holds both layouts of a
-70B TP8 shard many times over.  ``EMA_SKINNY_PACK=0`` streams the row-major
+The packed copies live next to the parameter (``_ema_decode_packed``, one per
+(GLU, half-tail) form, so the <= 16-row and 17-32-row decode forms do not
+evict each other) and are rebuilt when the parameter's storage, in-place
+version or the global weight generation changes.  The generation is bumped
+by every optimizer step and checkpoint load (:func:`bump_weight_generation`):
+those rewrite the weights through the DDP flat buffers, which does not move
+the Parameter's ``_version``.  288 GB of HBM holds both layouts of a 70B TP8
+shard many times over.  ``EMA_SKINNY_PACK=0`` streams the row-major
 weights instead (A/B).
 """
 import os
@@ -33,6 +37,17 @@ import os
 import torch
 
 ENABLED = os.environ.get("EMA_SKINNY_PACK", "1") != "0"
+_WEIGHT_GEN = [0]
+
+
+def bump_weight_generation():
+    """Weights may have been rewritten outside the Parameter objects
+    (optimizer step, checkpoint load): every packed copy is stale."""
+    _WEIGHT_GEN[0] += 1
+
+
+def weight_generation():
+    return _WEIGHT_GEN[0]
 
 
 def packable(w):
@@ -90,11 +105,18 @@ def packed(w, glu=False, half_tail=0):
     weight must be streamed (disabled / unsupported shape)."""
     if not ENABLED or not packable(w):
         return None
-    key = (w.data_ptr(), w._version, bool(glu), int(half_tail), w.dtype, tuple(w.shape))
-    hit = getattr(w, "_ema_decode_packed", None)
+    form = (bool(glu), int(half_tail))
+    key = (w.data_ptr(), w._version, _WEIGHT_GEN[0], w.dtype, tuple(w.shape))
+    cache = getattr(w, "_ema_decode_packed", None)
+    if not isinstance(cache, dict):
+        cache = {}
+        w._ema_decode_packed = cache
+    hit = cache.get(form)
     if hit is not None and hit[0] == key:
         return hit[1]
+    for f in [f for f, v in cache.items() if v[0] != key]:
+        del cache[f]  # stale forms of an older generation
     with torch.no_grad():
         p = pack(w.detach(), glu, half_tail)
-    w._ema_decode_packed = (key, p)
+    cache[form] = (key, p)
     return p

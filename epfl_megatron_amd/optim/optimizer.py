@@ -40,6 +40,7 @@ import math
 import torch
 import torch.distributed as dist
 
+from ..ops import decode_pack
 from ..parallel import state, comm
 from ..parallel.tensor.layers import param_is_not_tensor_parallel_duplicate
 from ..models.module import param_is_not_shared
@@ -449,6 +450,10 @@ class MegatronOptimizer:
             barrier=args.barrier_with_L1_time)
         self.gather_model_params(args, timers)
         timers("optimizer-copy-main-to-model-params").stop()
+        # parameters were rewritten through the flat buffers (not through the
+        # Parameter objects, whose _version does not move): invalidate the
+        # derived copies keyed on the weight generation (decode-packed weights)
+        decode_pack.bump_weight_generation()
         res = StepResult(self._st)
         self._pending = res
         return res, LazyScalar(lambda: (None if res.found_inf else res.grad_norm)), num_zeros
@@ -530,6 +535,7 @@ class MegatronOptimizer:
             self._push_master_to_model()
 
     def _push_master_to_model(self):
+        decode_pack.bump_weight_generation()
         for c in self.chunks:
             if c.model_out is not None:
                 K.copy_master_to_model(c.master, c.model_out, c.plan)

@@ -77,18 +77,28 @@ def set_loopback(group, world):
         _GROUP_SIZES[name] = int(world)
 
 
-def enable_xgmi_allreduce(group, cap_bytes):
-    """Route small sum all-reduces and all-gathers on ``group`` (contiguous
-    bf16 / fp16 / fp32 CUDA tensors of at most ``cap_bytes`` per rank) through
-    the one-shot xGMI kernel (``parallel/xgmi.py``); RCCL keeps everything else.  Collective over the
-    group (handle exchange).  ``cap_bytes`` 0 / None disables."""
+def enable_xgmi_allreduce(group, cap_bytes, gather_cap_bytes=None):
+    """Route sum all-reduces of at most ``cap_bytes`` and all-gathers of at
+    most ``gather_cap_bytes`` per rank (default: ``cap_bytes``) on ``group``
+    (contiguous bf16 / fp16 / fp32 CUDA tensors) through the one-shot xGMI
+    kernel (``parallel/xgmi.py``); RCCL keeps everything else.  Collective over
+    the group (handle exchange).  Both caps 0 / None disables."""
     old = _XGMI.pop(id(group), None)
     if old is not None:
         old.close()
-    if cap_bytes:
+    ag = cap_bytes if gather_cap_bytes is None else gather_cap_bytes
+    if cap_bytes or ag:
         from .xgmi import XgmiAllReduce  # noqa: PLC0415
-        _XGMI[id(group)] = XgmiAllReduce(group, cap_bytes)
+        _XGMI[id(group)] = XgmiAllReduce(group, cap_bytes or 0, ag or 0)
     return _XGMI.get(id(group))
+
+
+def check_xgmi():
+    """Raise :class:`parallel.xgmi.XgmiError` if any registered one-shot
+    collective timed out waiting for a peer (cheap: one 4-byte read per
+    communicator; synchronises the device)."""
+    for xg in _XGMI.values():
+        xg.check()
 
 
 def xgmi_allreduce_of(group):

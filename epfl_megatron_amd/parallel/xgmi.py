@@ -23,6 +23,18 @@ to RCCL, and ``comm.all_gather_into`` likewise the all-gathers whose
 per-rank message fits (e.g. the vocab-parallel decode logits).  Capturable in
 a hipGraph (epochs live on the device).
 
+Routing is decided from rank-uniform properties only (dtype, element count,
+contiguity): a rank whose tensor happens to be misaligned stages it through
+an aligned buffer instead of taking RCCL while its peers take the kernel (which
+would hang or time out).  All-reduces and all-gathers have separate caps
+(``--tp_xgmi_allreduce_kb`` / ``--tp_xgmi_allgather_kb``): the all-gather cap
+covers the multi-MiB sequence-parallel ``[s/tp, b, h]`` pieces.
+
+A wait on a peer is bounded by wall clock (``EMA_XGMI_TIMEOUT_MS``, default
+1000): a dead peer ends the kernel with NaN-filled output and the error word
+set, and :meth:`check` (called by every training log line and after every
+generate call) raises.
+
 Verified on one MI355X with 2 and 4 processes sharing the GPU
 (``tests/test_xgmi_gpu.py``: same-device IPC mappings; the flag / parity
 protocol and the kernel are the ones a multi-GPU run executes, the transport
@@ -48,10 +60,14 @@ class XgmiAllReduce:
 
     DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
-    def __init__(self, group=None, cap_bytes=1 << 20):
-        cap = int(cap_bytes)
-        if cap <= 0 or cap % 4096:
-            raise ValueError("cap_bytes must be a positive multiple of 4096")
+    def __init__(self, group=None, cap_bytes=1 << 20, gather_cap_bytes=None):
+        ar = int(cap_bytes)
+        ag = ar if gather_cap_bytes is None else int(gather_cap_bytes)
+        cap = max(ar, ag)
+        if cap <= 0 or ar % 4096 or ag % 4096 or ar < 0 or ag < 0:
+            raise ValueError("caps must be non-negative multiples of 4096 (one positive)")
+        self.ar_cap, self.ag_cap = ar, ag
+        self._stage = {}
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -66,25 +82,53 @@ class XgmiAllReduce:
         C.xgmi_open(self.id, table.view(self.world, -1))
         dist.barrier(group=group)
 
-    def eligible(self, t):
+    def _fits(self, t, cap):
+        # rank-uniform: dtype, size and contiguity agree across the TP group
+        # (never the address, which can differ per rank: ADVICE r4)
         nbytes = t.numel() * t.element_size()
-        return (t.is_cuda and t.dtype in self.DTYPES and t.is_contiguous() and 0 < nbytes <= self.cap
-                and nbytes % 16 == 0 and t.data_ptr() % 16 == 0)
+        return (t.is_cuda and t.dtype in self.DTYPES and t.is_contiguous() and 0 < nbytes <= cap
+                and nbytes % 16 == 0)
+
+    def eligible(self, t):
+        return self._fits(t, self.ar_cap)
+
+    def _aligned(self, t, key):
+        """``t`` itself when 16-B aligned, else a cached aligned staging copy."""
+        if t.data_ptr() % 16 == 0:
+            return t, False
+        buf = self._stage.get(key)
+        if buf is None or buf.numel() != t.numel() or buf.dtype != t.dtype or buf.device != t.device:
+            buf = torch.empty_like(t, memory_format=torch.contiguous_format)
+            self._stage[key] = buf
+        buf.copy_(t)
+        return buf, True
 
     def __call__(self, t, out=None):
         """``out`` (default: ``t``, in place) = sum of ``t`` over the group, on
         the current stream."""
-        _ext().xgmi_all_reduce(self.id, t, t if out is None else out)
-        return t if out is None else out
+        dst = t if out is None else out
+        src, _ = self._aligned(t, "ar_in")
+        if out is None or out.data_ptr() % 16:
+            o = src if out is None else self._aligned(out, "ar_out")[0]
+        else:
+            o = out
+        _ext().xgmi_all_reduce(self.id, src, o)
+        if o.data_ptr() != dst.data_ptr():
+            dst.copy_(o)
+        return dst
 
     def gather_eligible(self, out, inp):
-        return (self.eligible(inp) and out.is_cuda and out.dtype == inp.dtype and out.is_contiguous()
-                and out.numel() == self.world * inp.numel() and out.data_ptr() % 16 == 0)
+        return (self._fits(inp, self.ag_cap) and out.is_cuda and out.dtype == inp.dtype
+                and out.is_contiguous() and out.numel() == self.world * inp.numel())
 
     def all_gather(self, out, inp):
         """``out`` = concat over ranks of ``inp`` along dim 0 (``inp`` may be
         this rank's chunk of ``out``), on the current stream."""
-        _ext().xgmi_all_gather(self.id, inp, out, self.world)
+        src, _ = self._aligned(inp, "ag_in")
+        o, staged = self._aligned(out, "ag_out") if out.data_ptr() % 16 else (out, False)
+        _ext().xgmi_all_gather(self.id, src, o, self.world)
+        if staged:
+            out.copy_(o)
         return out
 
     def check(self):

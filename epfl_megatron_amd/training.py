@@ -28,7 +28,7 @@ from .parallel import state
 from .parallel.ddp import DistributedDataParallel as LocalDDP
 from .parallel.pipeline.schedules import get_forward_backward_func
 from .parallel.tensor import set_defaults_if_not_set_tensor_model_parallel_attributes
-from .parallel.tensor.layers import new_weight_transpose_generation
+from .parallel.tensor.layers import fallback_report, new_weight_transpose_generation
 from .utils.misc import (calc_params_l2_norm, check_adlr_autoresume_termination, print_all_nodes,
                          print_rank_0, print_rank_last, report_memory, unwrap_model)
 from .utils.flops import flops_per_token
@@ -385,6 +385,14 @@ def training_log(loss_dict, total_loss_dict, learning_rate, iteration, loss_scal
             report_memory(f"(after {iteration} iterations)")
             report_memory_flag = False
         timers.log(timers_to_log, normalizer=args.log_interval)
+        # correctness checks that run whatever the timing level: a one-shot
+        # xGMI collective that timed out produced NaN output (raise now), and
+        # GPU GEMMs that fell back to torch math are reported
+        comm.check_xgmi()
+        fb = fallback_report()
+        if fb:
+            print_rank_last(" GEMM kernel fallbacks (cumulative): " + ", ".join(
+                f"{k}: {v}" for k, v in fb.items()))
         if args.timing_log_level >= 1:
             rep = comm.report()
             if rep:

@@ -9,12 +9,13 @@
 # abort or a time limit).  Steps:
 #   tests      pytest -m gpu (one process)
 #   quick      pytest -m gpu on the kernel / GEMM numerics files only
+#   pyt        pytest -m gpu $PYTEST_ARGS (a chosen subset)
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py --steps 8 --warmup 2 (the headline config)
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
-#   wgrad      scripts/wgrad_bench.py
+#   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
 #   fa         scripts/fa_bench.py
 #   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
 #   px70       bench.py --proxy llama70b-tp8
@@ -58,12 +59,14 @@ for step in "$@"; do
              -p no:cacheprovider tests -m gpu ;;
     quick) run quick 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
              -p no:cacheprovider tests/test_kernels_gpu.py tests/test_gemm_gpu.py -m gpu ;;
+    pyt) run pyt 900 python -u -m pytest -x -q --timeout 280 --timeout-method thread \
+             -p no:cacheprovider -m gpu $PYTEST_ARGS ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 500 python -u bench.py --steps 8 --warmup 2 $BENCH_ARGS ;;
     prof) prof prof 600 python3 -u bench.py --steps 2 --warmup 1 $BENCH_ARGS ;;
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
-    gemm) run gemm 400 python -u scripts/gemm_nt_bench.py ;;
-    wgrad) run wgrad 400 python -u scripts/wgrad_bench.py ;;
+    gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
+    wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
     fa) run fa 400 python -u scripts/fa_bench.py ;;
     px7) run px7 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     px70) run px70 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;

@@ -156,12 +156,21 @@ def test_gpu_kv_cached_decode_matches_full_forward():
     assert err < 3e-2 * max(1.0, scale), (err, scale)
 
 
-def _decode_fused_vs_unfused(rank, world, b=3):
+# 70B-at-TP4-shaped layers (h 8192, ffn 7168 = 28672 / 4): K = 8192 takes the
+# persistent skinny kernels, whose un-normed GLU form has a non-zero half-unit
+# tail on 256 CUs (the tail must match the form that runs)
+LLAMA_H8K = [a for a in LLAMA_GQA]
+for _k, _v in (("--hidden_size", "8192"), ("--num_attention_heads", "64"),
+               ("--num_attention_heads_kv", "8"), ("--ffn_hidden_size", "7168")):
+    LLAMA_H8K[LLAMA_H8K.index(_k) + 1] = _v
+
+
+def _decode_fused_vs_unfused(rank, world, b=3, big=False):
     """The fused decode layer (5 weight-streaming launches with norm / RoPE /
     KV-cache write / GLU / residual inside, csrc/skinny_gemm.hip) against the
     unfused kernels on the same prefilled cache: logits and greedy tokens."""
     import finetune
-    init_framework(LLAMA_GQA + ["--bf16"], finetune.extra_args)
+    init_framework((LLAMA_H8K if big else LLAMA_GQA) + ["--bf16"], finetune.extra_args)
     from epfl_megatron_amd import get_args
     from epfl_megatron_amd.models import ModelType, transformer
     from epfl_megatron_amd.training import get_model
@@ -208,15 +217,16 @@ def _decode_fused_vs_unfused(rank, world, b=3):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("b", [3, 24])
-def test_gpu_fused_decode_matches_unfused(b):
-    """b = 24: 17-32 sequences run two 16-row blocks per weight fragment."""
-    calls, err, scale, tf, tu, cache_err = run_dist(_decode_fused_vs_unfused, 1, b)[0]
+@pytest.mark.parametrize("b,big", [(3, False), (24, False), (12, True), (24, True)])
+def test_gpu_fused_decode_matches_unfused(b, big):
+    """b = 24: 17-32 sequences run two 16-row blocks per weight fragment;
+    big: h = 8192 layers (persistent kernels, GLU half-unit tails)."""
+    calls, err, scale, tf, tu, cache_err = run_dist(_decode_fused_vs_unfused, 1, b, big)[0]
     assert calls == 2 * 8, calls  # every decode step of both layers took the fused path
     assert err < 2e-2 * max(1.0, scale), (err, scale)
-    if b <= 16:
+    if b <= 16 and not big:
         assert tf == tu
-    else:  # (24 x 8 greedy picks through two numerics paths: allow rare near-tie flips)
+    else:  # (24 x 8 / h 8192 greedy picks through two numerics paths: allow rare near-tie flips)
         same = sum(x == y for a, c in zip(tf, tu) for x, y in zip(a, c))
         assert same >= 0.9 * b * 8, (same, tf, tu)
     assert cache_err < 5e-2, cache_err

@@ -596,7 +596,7 @@ def test_skinny_packed_weights_match_row_major(M, N, K):
         assert torch.equal(C.skinny_gemm(x, wp, True), C.skinny_gemm(x, w))
         assert torch.equal(C.skinny_norm_gemm(x, wp, g, 1e-5, res, True),
                            C.skinny_norm_gemm(x, w, g, 1e-5, res))
-        tail = C.skinny_glu_half_tail(N // 2, K, True)
+        tail = C.skinny_glu_half_tail(N // 2, K, True, M)
         wg = decode_pack.pack(w, glu=True, half_tail=tail)
         assert torch.equal(decode_pack.unpack(wg, glu=True, half_tail=tail), w)
         for kind in (0, 1):

@@ -505,6 +505,46 @@ def test_decode_pack_layout():
     assert not dp.packable(torch.zeros(16, 512))
 
 
+def test_decode_pack_cache_generation():
+    """Packed copies are keyed on the global weight generation: a weight
+    rewritten through its flat buffer (the optimizer's path: ``p.data`` is a
+    view whose ``_version`` does not move) is repacked once the generation is
+    bumped; the <= 16-row and 17-32-row forms (different half-unit tails)
+    are cached side by side."""
+    from epfl_megatron_amd.ops import decode_pack as dp
+    flat = torch.randn(64 * 512).bfloat16()
+    w = torch.nn.Parameter(torch.empty(0, dtype=torch.bfloat16), requires_grad=False)
+    w.data = flat.view(64, 512)
+    a = dp.packed(w, glu=True, half_tail=1)
+    b = dp.packed(w, glu=True, half_tail=0)
+    assert dp.packed(w, glu=True, half_tail=1) is a and dp.packed(w, glu=True, half_tail=0) is b
+    with torch.no_grad():
+        flat.add_(1.0)  # rewrite through the buffer, as copy_master_to_model does
+    dp.bump_weight_generation()
+    a2 = dp.packed(w, glu=True, half_tail=1)
+    assert a2 is not a and torch.equal(a2, dp.pack(w.detach(), True, 1))
+
+
+def _train_two_steps(rank, world):
+    import finetune
+    argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "1"]
+    argv[argv.index("--train_iters") + 1] = "2"
+    init_framework(argv, finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.ops import decode_pack as dp
+    from epfl_megatron_amd.training import pretrain
+    g0 = dp.weight_generation()
+    pretrain(get_args(), finetune.train_valid_test_datasets_provider, finetune.model_provider,
+             ModelType.encoder_or_decoder, finetune.forward_step)
+    return dp.weight_generation() - g0
+
+
+def test_optimizer_step_bumps_weight_generation():
+    """Every optimizer step invalidates the derived weight copies."""
+    assert run_dist(_train_two_steps, 1)[0] >= 2
+
+
 # ------------------------------------------------- one-shot all-reduce routing
 class _FakeOneShot:
     """Stands in for parallel.xgmi.XgmiAllReduce on the CPU: eligible for

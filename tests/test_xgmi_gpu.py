@@ -137,6 +137,103 @@ def _rank(rank, world):
     return out
 
 
+def _rank_sp_gather(rank, world):
+    """(2 ranks: their two 1024-workgroup grids must be co-resident on the one
+    GPU of the test box; across GPUs there is no such limit.)
+    Multi-MiB all-gathers of sequence-parallel [s/tp, b, h] pieces through
+    the one-shot kernel (separate gather cap), checked against the process
+    group's own all_gather_into_tensor; misaligned tensors are staged (the
+    routing decision never depends on an address)."""
+    import torch.distributed as dist
+
+    from epfl_megatron_amd.parallel import comm
+    from epfl_megatron_amd.parallel.xgmi import XgmiAllReduce
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    grp = dist.group.WORLD
+    xg = XgmiAllReduce(grp, cap_bytes=64 * 1024, gather_cap_bytes=4 * 1024 * 1024)
+    comm._XGMI[id(grp)] = xg
+    bad = []
+    g = torch.Generator().manual_seed(11 + rank)
+    for it, (s, b, h) in enumerate(((512, 1, 4096), (256, 2, 2048), (128, 1, 4096))):
+        piece = torch.randn(s, b, h, generator=g).to(torch.bfloat16)
+        ref = torch.empty(world * s, b, h, dtype=torch.bfloat16)
+        dist.all_gather_into_tensor(ref, piece, group=grp)  # gloo oracle
+        out = torch.empty(world * s, b, h, dtype=torch.bfloat16, device="cuda")
+        comm.report(reset=True)
+        comm.all_gather_into(out, piece.cuda(), group=grp)
+        torch.cuda.synchronize()
+        rep = comm.report()
+        if not any(k.startswith("all_gather_xgmi") for k in rep):
+            bad.append(("not routed", it, sorted(rep)))
+        if not torch.equal(out.cpu(), ref):
+            bad.append(("sp gather", it))
+    # all-reduce above its own cap goes to the process group even though the
+    # registered region is larger (the gather cap)
+    big = torch.ones(256 * 1024, dtype=torch.float32, device="cuda")
+    comm.report(reset=True)
+    comm.all_reduce(big, group=grp)
+    torch.cuda.synchronize()
+    if any(k.startswith("all_reduce_xgmi") for k in comm.report()) or not torch.all(big == world):
+        bad.append("all-reduce cap")
+    # a tensor at an odd byte offset (rank-dependent alignment) is staged
+    raw = torch.zeros(4096 + 8 * rank + 1, dtype=torch.bfloat16, device="cuda")
+    t = raw[1 + 8 * rank: 1 + 8 * rank + 4096]
+    t.fill_(float(rank + 1))
+    comm.all_reduce(t, group=grp)
+    torch.cuda.synchronize()
+    if not torch.all(t.cpu() == float(sum(range(1, world + 1)))):
+        bad.append("misaligned all-reduce")
+    comm._XGMI.pop(id(grp))
+    xg.check()
+    dist.barrier()
+    xg.close()
+    return bad
+
+
+def _rank_dead_peer(rank, world):
+    """Rank 1 never joins: rank 0's call ends after EMA_XGMI_TIMEOUT_MS with a
+    NaN-filled output, and check() raises (no hang, no stale sums)."""
+    import time
+
+    import torch.distributed as dist
+
+    from epfl_megatron_amd.parallel.xgmi import XgmiAllReduce, XgmiError
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    xg = XgmiAllReduce(None, cap_bytes=64 * 1024)
+    res = None
+    if rank == 0:
+        t = torch.ones(8192, dtype=torch.bfloat16, device="cuda")
+        t0 = time.perf_counter()
+        xg(t)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        try:
+            xg.check()
+            raised = False
+        except XgmiError:
+            raised = True
+        res = (bool(torch.isnan(t.float()).all().item()), raised, dt)
+    dist.barrier()
+    xg.close()
+    return res
+
+
+def test_xgmi_sp_piece_allgather():
+    for bad in run_dist(_rank_sp_gather, 2, timeout=300):
+        assert not bad, bad
+
+
+def test_xgmi_dead_peer_times_out():
+    res = run_dist(_rank_dead_peer, 2, timeout=300, env={"EMA_XGMI_TIMEOUT_MS": "300"})
+    all_nan, raised, dt = res[0]
+    assert all_nan and raised
+    assert dt < 5.0, dt  # bounded by the 300 ms wall-clock wait, not tens of seconds
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_xgmi_oneshot_allreduce(world):
     res = run_dist(_rank, world, timeout=300)
