@@ -41,7 +41,6 @@ _GROUP_NAMES = {}
 _GROUP_SIZES = {}  # name -> ranks in the group (bus-bandwidth factors of the report)
 _PENDING_EVENTS = []  # (key, start_event, end_event) not yet folded into _STATS
 _LOOPBACK = {}  # id(group) -> simulated size (--simulated_tensor_parallel_size)
-_LOOPBACK_FILLED = set()  # (data_ptr, numel) of all-gather outputs zero-filled once
 _XGMI = {}  # id(group) -> parallel.xgmi.XgmiAllReduce (one-shot small all-reduce)
 
 
@@ -306,13 +305,15 @@ def all_gather_into(output, inp, group=None, async_op=False):
     n = _LOOPBACK.get(id(group))
     if n:
         def loop(a):
-            key = (output.data_ptr(), output.numel())
-            if key not in _LOOPBACK_FILLED:
-                _LOOPBACK_FILLED.add(key)
-                output.zero_()
-            own = output.view(n, *src.shape)[0]
-            if own.data_ptr() != src.data_ptr():
-                own.copy_(src)
+            # every simulated peer's slot gets this rank's shard: the output is
+            # fully written each call (as a real all-gather writes it), so no
+            # stale / non-finite bytes of a recycled allocation reach the loss
+            # (ADVICE r4), and the proxy's write traffic matches a real rank's
+            rows = output.view(n, -1)
+            flat = src.reshape(1, -1)
+            if rows[0].data_ptr() != src.data_ptr():
+                rows[0:1].copy_(flat)
+            rows[1:].copy_(flat.expand(n - 1, -1))
         return _issue("all_gather", group, output, src, loop, async_op)
     xg = _XGMI.get(id(group))
     if xg is not None and xg.gather_eligible(output, src):

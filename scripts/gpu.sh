@@ -13,6 +13,7 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py --steps 8 --warmup 2 (the headline config)
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
+#   profpx7    rocprofv3 kernel trace of the llama7b-tp8 proxy (profpx70: llama70b-tp8)
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
@@ -64,6 +65,8 @@ for step in "$@"; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 500 python -u bench.py --steps 8 --warmup 2 $BENCH_ARGS ;;
     prof) prof prof 600 python3 -u bench.py --steps 2 --warmup 1 $BENCH_ARGS ;;
+    profpx7) prof profpx7 600 python3 -u bench.py --proxy llama7b-tp8 --steps 2 --warmup 1 ;;
+    profpx70) prof profpx70 900 python3 -u bench.py --proxy llama70b-tp8 --steps 1 --warmup 1 ;;
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;

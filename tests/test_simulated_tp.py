@@ -21,9 +21,10 @@ def _sim_rank(rank, world, n):
     x = torch.arange(6, dtype=torch.float32).view(3, 2)
     full = torch.empty(3 * n, 2)
     comm.all_gather_into(full, x, group=g)
-    # emulation moves only this rank's own bytes: own slot written, the other
-    # ranks' slots zero-filled once (finite stand-ins), no reduction kernel
-    out["ag"] = torch.equal(full[:3], x) and not full[3:].any()
+    # emulation: every simulated rank's slot holds this rank's shard (finite
+    # stand-ins written on every call, as a real all-gather writes its whole
+    # output), no reduction kernel
+    out["ag"] = all(torch.equal(full[3 * i:3 * i + 3], x) for i in range(n))
     parts = torch.arange(n * 6, dtype=torch.float32).view(n * 3, 2)
     rs = torch.empty(3, 2)
     comm.reduce_scatter_into(rs, parts, group=g)
