@@ -983,13 +983,6 @@ std::vector<int64_t> wgrad_plan(int64_t M, int64_t N, int64_t K) {
   return {p.main_tiles, p.tail_lin0, p.tail_tiles, p.nsplit};
 }
 
-void wgrad_gemm_ablation(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, int64_t mode) {
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "ablation builds are bf16 only");
-  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
-  TORCH_CHECK(ema::wgrad_supported(M, N, K) && g.numel() == N * K, "unsupported shape");
-  ema::wgrad_gemm_ablation(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), M, N, K, (int)mode,
-                           cur_stream());
-}
 
 // ---------------------------------------------------------------- NT GEMM
 // 2-D, row stride multiple of 8 elements, unit column stride, 16-B aligned
@@ -1199,7 +1192,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
   m.def("wgrad_gemm", &wgrad_gemm);
   m.def("wgrad_supported", &wgrad_supported);
-  m.def("wgrad_gemm_ablation", &wgrad_gemm_ablation);
   m.def("wgrad_set_variant", &ema::wgrad_set_variant);
   m.def("gemm_lab", [](const at::Tensor& a, const at::Tensor& b, at::Tensor c, int64_t variant) {
     TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&

@@ -106,7 +106,7 @@ struct VPlan {
   int rd0[16];   // next step's k-half-0 reads
   int b1, b2, w;
 };
-constexpr VPlan kVPlan[5] = {
+constexpr VPlan kVPlan[7] = {
     {{0, 2, 4, 6, 8, 10, 12, 14, 24, 27, 30, 33, 36, 38, 40, 42},
      {22, 25, 28, 31, 34, 52, 55, 58, 61, 64, 85, 87, 89, 96, 100, 124},
      {93, 94, 95, 97, 98, 102, 103, 104, 105, 106, 109, 112, 114, 117, 120, 123},
@@ -130,6 +130,17 @@ constexpr VPlan kVPlan[5] = {
      {22, 25, 28, 31, 34, 52, 55, 58, 61, 64, 85, 87, 89, 104, 108, 124},
      {101, 102, 103, 105, 106, 108, 109, 110, 111, 112, 113, 115, 116, 118, 120, 123},
      20, 50, 99},
+    // 5: two barriers per K-step: all 16 k-half-1 reads before barrier 1, all
+    //    16 pieces after it (every 4 MFMAs), wait at 95
+    {{0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30},
+     {34, 38, 42, 46, 50, 54, 58, 62, 66, 70, 74, 78, 82, 86, 90, 94},
+     {96, 98, 100, 102, 104, 106, 108, 110, 112, 114, 116, 118, 120, 122, 124, 126},
+     32, -1, 95},
+    // 6: as 5 with the pieces every 3 MFMAs (34..79)
+    {{0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30},
+     {34, 37, 40, 43, 46, 49, 52, 55, 58, 61, 64, 67, 70, 73, 76, 79},
+     {96, 98, 100, 102, 104, 106, 108, 110, 112, 114, 116, 118, 120, 122, 124, 126},
+     32, -1, 95},
 };
 constexpr int vplan_vmw(int par) {
   int n = 0;
@@ -425,6 +436,8 @@ void gemm_lab(const void* a, const void* b, void* c, int64_t M, int64_t N, int64
   else if (variant == 10) hipLaunchKernelGGL((lab_nt_k<0, 3>), dim3(g), dim3(256), 0, s, p);
   else if (variant == 11) hipLaunchKernelGGL((lab_nt_k<0, 4>), dim3(g), dim3(256), 0, s, p);
   else if (variant == 12) hipLaunchKernelGGL((lab_nt_k<0, 5>), dim3(g), dim3(256), 0, s, p);
+  else if (variant == 13) hipLaunchKernelGGL((lab_nt_k<0, 6>), dim3(g), dim3(256), 0, s, p);
+  else if (variant == 14) hipLaunchKernelGGL((lab_nt_k<0, 7>), dim3(g), dim3(256), 0, s, p);
   else if (variant == 9) hipLaunchKernelGGL((lab_nt_k<3, 1>), dim3(g), dim3(256), 0, s, p);
   else if (variant == 4) hipLaunchKernelGGL((lab_nt_k<0, 1>), dim3(g), dim3(256), 0, s, p);
   else if (variant == 5) hipLaunchKernelGGL((lab_nt_k<0, 2>), dim3(g), dim3(256), 0, s, p);

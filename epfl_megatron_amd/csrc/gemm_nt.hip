@@ -772,7 +772,7 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
       for (int jp = 0; jp < 4; ++jp) {
         const uint4 v = pair_to_row8(pack4<T>(acc[ii][2 * jp]), pack4<T>(acc[ii][2 * jp + 1]));
         const int64_t col = gn0 + 32 * jp + 8 * q;
-        if (rok && col < N) *reinterpret_cast<uint4*>(c + row * p.ldc + col) = v;
+        if (rok && col < N) *reinterpret_cast<uint4*>(c + map_row(row, p.cm) * p.ldc + col) = v;
       }
     } else if constexpr (EPI == EPI_GLU) {
       T* pre = reinterpret_cast<T*>(p.c);
@@ -792,23 +792,39 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
         const uint4 vy = pair_to_row8(yy[0], yy[1]);
         const int64_t f = gn0 + 32 * jp + 8 * q;
         if (rok && f < N) {
-          *reinterpret_cast<uint4*>(pre + row * p.ldc + f) = vu;
-          *reinterpret_cast<uint4*>(pre + row * p.ldc + N + f) = vg;
-          *reinterpret_cast<uint4*>(y + row * p.ldy + f) = vy;
+          const int64_t pr = map_row(row, p.cm);
+          *reinterpret_cast<uint4*>(pre + pr * p.ldc + f) = vu;
+          *reinterpret_cast<uint4*>(pre + pr * p.ldc + N + f) = vg;
+          *reinterpret_cast<uint4*>(y + pr * p.ldy + f) = vy;
         }
       }
-    } else {
-      const T* pre = reinterpret_cast<const T*>(p.pre);
-      T* d = reinterpret_cast<T*>(p.c);
-      const int64_t rr = rok ? row : M - 1;
-      V x1[4], x2[4];
+    }
+  }
+  if constexpr (EPI == EPI_DGLU) {
+    // d(pre) from dAct (rounded to T) and the saved pre-activation, software-
+    // pipelined over the 8 row groups: the pre loads of D groups are in flight
+    // while a group computes and stores (the epilogue was latency-bound: one
+    // group's 8 loads at a time)
+    const T* pre = reinterpret_cast<const T*>(p.pre);
+    T* d = reinterpret_cast<T*>(p.c);
+    constexpr int D = 3;
+    V x1[D][4], x2[D][4];
+    auto load = [&](int ii, V (&a)[4], V (&b)[4]) {
+      const int64_t row = gm0 + 16 * ii + (lane & 15);
+      const int64_t rr = row < M ? row : M - 1;
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
         int64_t f = gn0 + 32 * jp + 8 * q;
         f = f < N ? f : 0;
-        x1[jp] = ld16(pre + rr * p.ldc + f);
-        x2[jp] = ld16(pre + rr * p.ldc + N + f);
+        a[jp] = ld16(pre + rr * p.ldc + f);
+        b[jp] = ld16(pre + rr * p.ldc + N + f);
       }
+    };
+    static_for<D>([&](auto k) { load(decltype(k)::value, x1[decltype(k)::value], x2[decltype(k)::value]); });
+    static_for<8>([&](auto iic) {
+      constexpr int ii = decltype(iic)::value, sl = ii % D;
+      const int64_t row = gm0 + 16 * ii + (lane & 15);
+      const bool rok = row < M;
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
         const uint4 gv = pair_to_row8(pack4<T>(acc[ii][2 * jp]), pack4<T>(acc[ii][2 * jp + 1]));
@@ -816,9 +832,9 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
         V da, dg;
 #pragma unroll
         for (int e = 0; e < V::N; ++e) {
-          const float gf = to_f(g.v[e]), xg = to_f(x2[jp].v[e]);
+          const float gf = to_f(g.v[e]), xg = to_f(x2[sl][jp].v[e]);
           da.v[e] = from_f<T>(gf * act<ACT>(xg));
-          dg.v[e] = from_f<T>(gf * to_f(x1[jp].v[e]) * dact<ACT>(xg));
+          dg.v[e] = from_f<T>(gf * to_f(x1[sl][jp].v[e]) * dact<ACT>(xg));
         }
         const int64_t f = gn0 + 32 * jp + 8 * q;
         if (rok && f < N) {
@@ -826,7 +842,8 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
           st16(d + row * p.ldc + N + f, dg);
         }
       }
-    }
+      if constexpr (ii + D < 8) load(ii + D, x1[sl], x2[sl]);
+    });
   }
 }
 
@@ -875,12 +892,17 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
     int64_t m0 = 0, n0 = 0;
     int64_t na = 0, nb = 0;
+    int64_t am0 = 0;
     if (i < nmine) {
       tile_org(i, m0, n0);
-      na = (int64_t)(M - m0) * p.lda * (int64_t)sizeof(T);
+      // a row map's groups hold whole 256-row tiles (host-checked): the tile's
+      // physical rows are contiguous from map_row(m0)
+      am0 = map_row(m0, p.am);
+      const int64_t arows = p.am.rows == 0 ? M - m0 : min((int64_t)TM, (int64_t)M - m0);
+      na = arows * p.lda * (int64_t)sizeof(T);
       nb = (int64_t)((EPI == EPI_GLU ? 2 * (int64_t)N : N) - n0) * p.ldb * (int64_t)sizeof(T);
     }
-    const char* a = reinterpret_cast<const char*>(p.a) + m0 * p.lda * (int64_t)sizeof(T);
+    const char* a = reinterpret_cast<const char*>(p.a) + am0 * p.lda * (int64_t)sizeof(T);
     const char* b = reinterpret_cast<const char*>(p.b) + n0 * p.ldb * (int64_t)sizeof(T);
     ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, (int)min(na, (int64_t)0x7fffffff), 0x00020000);
     rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)min(nb, (int64_t)0x7fffffff), 0x00020000);
@@ -1036,9 +1058,13 @@ void launch_one(const NtArgs& p, hipStream_t s) {
   if constexpr (!(EPI == EPI_DGLU && ACT == 1)) {
     const int64_t lim = (int64_t)1 << 31;
     const int64_t brows = EPI == EPI_GLU ? 2 * (int64_t)p.N : p.N;
-    if (g_var[EPI] == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 &&
-        p.am.rows == 0 && p.cm.rows == 0 &&
-        (int64_t)p.M * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
+    // row maps: the persistent kernel reads a mapped A tile as one contiguous
+    // block, so the map's groups must hold whole 256-row tiles (the SP
+    // pipeline's pieces do at the BASELINE sizes: 512-1024 rows)
+    const bool maps_ok = (p.am.rows == 0 || p.am.rows % TM == 0) && (p.cm.rows == 0 || p.cm.rows % TM == 0);
+    const int64_t a_extent = p.am.rows == 0 ? (int64_t)p.M : (int64_t)TM;  // rows one descriptor spans
+    if (g_var[EPI] == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 && maps_ok &&
+        a_extent * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
       const int g = std::min(p.ntm * p.ntn, num_cus());
       hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, p);
       return;

@@ -26,16 +26,15 @@
 //   * Ping-pong: waves 4..7 run one barrier behind waves 0..3 (two barriers
 //     per phase), so on every SIMD one wave's 32 MFMAs (s_setprio 1) overlap
 //     the other wave's fragment reads.  The 4 DMA pieces of subtile p+3 are
-//     split between the two sections (SCHED 5, the production schedule): dY's
-//     two and X's first in the load section after the fragment reads, X's
-//     second inside the MFMA section.  Each glds costs ~60 issue cycles: all
-//     four in the load section made it the critical path (SCHED 0, fc1
-//     1.09-1.16 PF), all four in the MFMA section stall the MFMA pipe (SCHED
-//     2, 1.25-1.32 PF), one per alternate MFMA row likewise (SCHED 4); splits
-//     of 1 / 2 / 3 pieces in the load section (SCHED 6 / 3 / 5): 1.31-1.44 /
-//     1.34-1.47 / 1.37-1.48 PF on fc1 / qkv / fc2 (profiles/r2f_wgrad_sched.txt,
-//     profiles/r2g_wgrad_sched.txt).  SCHED 1, a non-ping-pong schedule with
-//     the reads between the MFMAs: 1.06-1.08 PF.
+//     split between the two sections: dY's two and X's first in the load
+//     section after the fragment reads, X's second inside the MFMA section.
+//     Each glds costs ~60 issue cycles; the alternatives measured in round 2
+//     (and removed since): all four in the load section made it the critical
+//     path (fc1 1.09-1.16 PF), all four in the MFMA section stall the MFMA
+//     pipe (1.25-1.32 PF), one per alternate MFMA row likewise; splits of 1 / 2
+//     / 3 pieces in the load section: 1.31-1.44 / 1.34-1.47 / 1.37-1.48 PF on
+//     fc1 / qkv / fc2 (profiles/r2f_wgrad_sched.txt, r2g_wgrad_sched.txt); a
+//     non-ping-pong schedule with the reads between the MFMAs: 1.06-1.08 PF.
 //   * Epilogue: fp32 read-modify-write of G (beta = 1) or plain store (beta =
 //     0: the first micro-batch of a step; main_grad is never zero-filled),
 //     transposed through LDS so G moves in 16-B row pieces (+1.5 % on fc1
@@ -143,7 +142,7 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
   else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
+template <typename T, bool ACCUM>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
         int K, int gn, int msplit, float* __restrict__ ws, int lin0, int nlin) {
@@ -195,18 +194,18 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
 
   auto stage = [&](int t) {  // slot t % NSLOT <- tokens [t*BM, t*BM + BM)
-    if constexpr (MODE == 2) return;  // ablation: no HBM/L2 traffic in the main loop
     const int dst = (t % NSLOT) * SLOTB;
     stage_op<T>(dy, N, (int64_t)t * BM, n0, lds, dst, wave, lane);
     stage_op<T>(x, K, (int64_t)t * BM, k0, lds, dst + OPB, wave, lane);
   };
 
   const int nt = M / BM;
-  // SCHED 3 / 5 / 6: 2 / 3 / 1 of a subtile's 4 DMA pieces (dY 0, dY 1, X 0,
-  // X 1) in the load section, the rest inside the MFMA section
-  constexpr int SPLITL = SCHED == 3 ? 2 : (SCHED == 5 || SCHED >= 7) ? 3 : SCHED == 6 ? 1 : 0;
-  // MFMA row after which the MFMA-section pieces issue (SCHED 7 / 8: rows 0 / 6)
-  constexpr int MROW = SCHED == 7 ? 0 : SCHED == 8 ? 6 : 3;
+  // Each glds costs ~60 issue cycles: 3 of a subtile's 4 DMA pieces (dY 0,
+  // dY 1, X 0) issue in the load section, X's second inside the MFMA section
+  // after MFMA row 3 (all four in the load section made it the critical path,
+  // 1.09-1.16 PF on fc1; all four among the MFMAs stalled the pipe, 1.25-1.32;
+  // 3 + 1: 1.37-1.48 PF, profiles/r2f_wgrad_sched.txt, r2g_wgrad_sched.txt)
+  constexpr int SPLITL = 3, MROW = 3;
   auto stage_piece = [&](int q, int ts) {
     const int dst = (ts % NSLOT) * SLOTB;
     if (q == 0) stage_op<T, 0, 1>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
@@ -214,7 +213,6 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     else if (q == 2) stage_op<T, 0, 1>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
     else stage_op<T, 1, 2>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
   };
-  if constexpr (SCHED != 1) {
   typename fa::MT<T>::x4 fa_[FA_][2], fb_[FB_][2];
   auto reads = [&](int t) {  // all fragments of subtile t (24 transposed reads)
     const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
@@ -248,38 +246,11 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
       constexpr int I = decltype(i)::value;
 #pragma unroll
       for (int j = 0; j < FB_; ++j) acc[I][j] = mfma16<T>(av[I], bv[j], acc[I][j]);
-      // SCHED 2: the DMA of subtile t+3 rides in the MFMA section (rows 1, 5)
-      // SCHED 3: only X's half does (row 3); dY's was issued in the load section
-      // SCHED 4: one DMA instruction per MFMA row 0, 2, 4, 6
-      if constexpr (SPLITL > 0 && MODE != 2 && I == MROW) {
+      if constexpr (I == MROW) {  // X's second DMA piece of subtile t+3 rides here
         const int ts = t + NSLOT - 1;
         if (ts < nt) {
           __builtin_amdgcn_sched_barrier(0);
           static_for<4 - SPLITL>([&](auto q) { stage_piece(SPLITL + decltype(q)::value, ts); });
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr (SCHED == 4 && MODE != 2 && (I % 2 == 0)) {
-        const int ts = t + NSLOT - 1;
-        if (ts < nt) {
-          __builtin_amdgcn_sched_barrier(0);
-          constexpr int P = (I / 2) & 1;
-          if constexpr (I < 4)
-            stage_op<T, P, P + 1>(dy, N, (int64_t)ts * BM, n0, lds, (ts % NSLOT) * SLOTB, wave, lane);
-          else
-            stage_op<T, P, P + 1>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave,
-                                  lane);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr (SCHED == 2 && MODE != 2 && (I == 1 || I == 5)) {
-        const int ts = t + NSLOT - 1;
-        if (ts < nt) {
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (I == 1)
-            stage_op<T>(dy, N, (int64_t)ts * BM, n0, lds, (ts % NSLOT) * SLOTB, wave, lane);
-          else
-            stage_op<T>(x, K, (int64_t)ts * BM, k0, lds, (ts % NSLOT) * SLOTB + OPB, wave, lane);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -294,31 +265,20 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   __builtin_amdgcn_s_barrier();            // ... and everyone's
   if (wn == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
 
-  // Phase p: [reads p][stage p+3][vmcnt: p+1 landed][lgkmcnt(0)] BAR_A
-  //          [32 MFMA] BAR_B
+  // Phase p: [reads p][3 DMA pieces of p+3][vmcnt: p+1 landed][lgkmcnt(0)] BAR_A
+  //          [32 MFMA + the 4th DMA piece of p+3] BAR_B
   // Group 0's BAR_A(p) is barrier 2p+1, group 1's is 2p+2 (= group 0's
   // BAR_B(p)): each group's MFMA section overlaps the other's load section.
   // RAW: subtile p+1 is retired by every wave before its BAR_A(p); both
   //      groups read it only after a later barrier.
   // WAR: stage(p+3) overwrites subtile p-1, whose reads every wave retired
   //      (lgkmcnt(0)) before its BAR_A(p-1), a barrier both groups passed.
-  // SCHED 2 issues stage(p+3) after BAR_A(p) instead (still after the
-  // retirement of subtile p-1's reads), so one subtile fewer is in flight at
-  // the vmcnt of the load section.
   for (int t = 0; t < nt; ++t) {
     reads(t);
-    if constexpr (SCHED == 0) {
-      if (t + NSLOT - 1 < nt) stage(t + NSLOT - 1);
-      wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 1));
-    } else if constexpr (SPLITL > 0) {
+    if (t + NSLOT - 1 < nt) {
       // the first SPLITL DMA pieces of subtile t+3 here (behind subtile t+2's 4)
-      if (t + NSLOT - 1 < nt) {
-        if constexpr (MODE != 2)
-          static_for<SPLITL>([&](auto q) { stage_piece(decltype(q)::value, t + NSLOT - 1); });
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 + SPLITL) : "memory");
-      } else {
-        wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
-      }
+      static_for<SPLITL>([&](auto q) { stage_piece(decltype(q)::value, t + NSLOT - 1); });
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 + SPLITL) : "memory");
     } else {
       wait_subtiles(min(t + NSLOT - 2, nt - 1) - (t + 1));
     }
@@ -331,82 +291,6 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   }
   if (wn == 0) __builtin_amdgcn_s_barrier();  // balance the barrier count
 
-  } else {
-    // SCHED 1: no ping-pong, one barrier per phase.  Phase p runs the 32
-    // MFMAs of subtile p (fragments read during phase p-1) interleaved with
-    // the 24 transposed reads of subtile p+1 and the DMA of subtile p+3.
-    // RAW: subtile p+1 is retired (counted vmcnt) by every wave before the
-    //      barrier that ends phase p-1.
-    // WAR: stage(p+3) overwrites subtile p-1, read during phase p-2 and
-    //      retired (lgkmcnt(0)) before the barrier ending phase p-2.
-    typename fa::MT<T>::x4 fr[2][FA_ + FB_][2];
-    auto rd = [&](auto set, int t, auto f) {  // fragment f (A: 0..7, B: 8..11) of subtile t
-      constexpr int S = decltype(set)::value, F = decltype(f)::value;
-      const uint32_t so = lds_base + (uint32_t)((t % NSLOT) * SLOTB);
-      if constexpr (F < FA_) {
-        fr[S][F][0] = fa::tr_read_imm<512 * (F >> 1), T>(so + abase[F & 1][0]);
-        fr[S][F][1] = fa::tr_read_imm<512 * (F >> 1), T>(so + abase[F & 1][1]);
-      } else {
-        constexpr int G = F - FA_;
-        fr[S][F][0] = fa::tr_read_imm<512 * (G >> 1), T>(so + bbase[G & 1][0]);
-        fr[S][F][1] = fa::tr_read_imm<512 * (G >> 1), T>(so + bbase[G & 1][1]);
-      }
-    };
-    auto phase = [&](auto cur, int t) {
-      constexpr int C = decltype(cur)::value, NX = 1 - C;
-      const bool more = t + 1 < nt, stg = t + NSLOT - 1 < nt;
-      typename fa::MT<T>::x8 bv[FB_];
-      static_for<FB_>([&](auto j) { bv[j] = fa::join<T>(fr[C][FA_ + j][0], fr[C][FA_ + j][1]); });
-      static_for<FA_>([&](auto i) {
-        constexpr int I = decltype(i)::value;
-        const typename fa::MT<T>::x8 av = fa::join<T>(fr[C][I][0], fr[C][I][1]);
-        __builtin_amdgcn_sched_barrier(0);
-        // the next subtile's 12 fragments over the 8 MFMA rows: row I reads
-        // A fragment I, rows 0-3 also B fragment I; rows 1 and 5 issue the DMA
-        if (more) {
-          rd(std::integral_constant<int, NX>{}, t + 1, std::integral_constant<int, I>{});
-          if constexpr (I < FB_) rd(std::integral_constant<int, NX>{}, t + 1,
-                                    std::integral_constant<int, FA_ + I>{});
-        }
-        if constexpr (I == 1 && MODE != 2) { if (stg) stage_op<T>(dy, N, (int64_t)(t + NSLOT - 1) * BM, n0, lds,
-                                                     ((t + NSLOT - 1) % NSLOT) * SLOTB, wave, lane); }
-        if constexpr (I == 5 && MODE != 2) { if (stg) stage_op<T>(x, K, (int64_t)(t + NSLOT - 1) * BM, k0, lds,
-                                                     ((t + NSLOT - 1) % NSLOT) * SLOTB + OPB, wave, lane); }
-        __builtin_amdgcn_sched_barrier(0);
-        static_for<FB_>([&](auto j) { acc[I][j] = mfma16<T>(av, bv[j], acc[I][j]); });
-      });
-      __builtin_amdgcn_sched_barrier(0);
-      wait_subtiles(min(t + NSLOT - 1, nt - 1) - (t + 2));  // subtile t+2 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-#pragma unroll
-    for (int t = 0; t < NSLOT - 1; ++t)
-      if (t < nt) stage(t);
-    wait_subtiles(min(nt, NSLOT - 1) - 2);  // subtiles 0 and 1 landed (own DMA)
-    __builtin_amdgcn_s_barrier();
-    static_for<FA_ + FB_>([&](auto f) { rd(std::integral_constant<int, 0>{}, 0, f); });
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    int t = 0;
-    for (; t + 1 < nt; t += 2) {
-      phase(std::integral_constant<int, 0>{}, t);
-      phase(std::integral_constant<int, 1>{}, t + 1);
-    }
-    if (t < nt) phase(std::integral_constant<int, 0>{}, t);
-  }
-
-  // epilogue: G[n][k] (+)= acc; lane holds col lane&15, rows 4(lane>>4) + r
-  if constexpr (MODE == 1) {  // ablation: keep acc alive, skip the epilogue traffic
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < FA_; ++i)
-#pragma unroll
-      for (int j = 0; j < FB_; ++j) s += acc[i][j][0] + acc[i][j][3];
-    if (s == 1234567.f) g[threadIdx.x] = s;
-    return;
-  }
   // Through LDS (free now: every ring read was retired before the last
   // barrier, no DMA is in flight): each wave transposes its 128 x 64 fp32
   // tile in two 64-row halves through a private 16 KiB region, so G moves
@@ -688,13 +572,13 @@ int tile_group(int ntn, int ntk) {
   return ntn >= ntk ? -4 : 8;
 }
 
-template <typename T, bool ACCUM, int MODE = 0, int SCHED = 0>
+template <typename T, bool ACCUM>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
             int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1) {
   const int ntiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
   if (nlin < 0) nlin = ntiles;
   const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
-  hipLaunchKernelGGL((wgrad_k<T, ACCUM, MODE, SCHED>), dim3(nlin * nsplit), dim3(512), 0, s,
+  hipLaunchKernelGGL((wgrad_k<T, ACCUM>), dim3(nlin * nsplit), dim3(512), 0, s,
                      (const T*)dy, (const T*)x, g, M, N, K,
                      tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), msplit,
                      nsplit > 1 ? ws : nullptr, lin0, nlin);
@@ -722,39 +606,6 @@ __global__ __launch_bounds__(256) void wgrad_split_reduce_k(const float* __restr
 
 }  // namespace
 
-// Ablation builds for profiling (bf16, accumulate): mode % 10 = 1 no epilogue
-// traffic, 2 no global loads in the main loop; mode / 10 = schedule variant.
-void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
-                         int64_t K, int mode, hipStream_t s) {
-  const int m = mode % 10, v = mode / 10;
-  const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (v == 7) {
-    launch<bf16, true, 0, 7>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 8) {
-    launch<bf16, true, 0, 8>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 5) {
-    launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 6) {
-    launch<bf16, true, 0, 6>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 3) {
-    launch<bf16, true, 0, 3>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 4) {
-    launch<bf16, true, 0, 4>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 2) {
-    if (m == 1) launch<bf16, true, 1, 2>(dy, x, g, iM, iN, iK, s);
-    else if (m == 2) launch<bf16, true, 2, 2>(dy, x, g, iM, iN, iK, s);
-    else launch<bf16, true, 0, 2>(dy, x, g, iM, iN, iK, s);
-  } else if (v == 1) {
-    if (m == 1) launch<bf16, true, 1, 1>(dy, x, g, iM, iN, iK, s);
-    else if (m == 2) launch<bf16, true, 2, 1>(dy, x, g, iM, iN, iK, s);
-    else launch<bf16, true, 0, 1>(dy, x, g, iM, iN, iK, s);
-  } else {
-    if (m == 1) launch<bf16, true, 1, 0>(dy, x, g, iM, iN, iK, s);
-    else if (m == 2) launch<bf16, true, 2, 0>(dy, x, g, iM, iN, iK, s);
-    else launch<bf16, true, 0, 0>(dy, x, g, iM, iN, iK, s);
-  }
-}
-
 bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
   return M > 0 && N >= 8 && K >= 8 && M % BM == 0 && N % 8 == 0 && K % 8 == 0 &&
          M <= (int64_t)1 << 30 && ((N + TN - 1) / TN) * ((K + TK - 1) / TK) < (int64_t)1 << 31 &&
@@ -762,38 +613,50 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 // Split planning (wgrad_plan).  One workgroup owns a 256 x 256 output tile,
-// so a grid that is not a multiple of the 256 CUs ends in a partial round.
-//   * fewer tiles than CUs (TP-sharded projections): split every tile's
-//     tokens over up to 8 workgroups;
-//   * a partial last round of at most 128 tiles (e.g. the 7B fc1 wgrad:
-//     1376 tiles = 5 rounds + 96): the full rounds run unsplit and only the
-//     tail tiles are split over the idle CUs.
-// At least 2048 tokens (64 ring subtiles) per split.
-WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K) {
-  const int tiles = (int)(((N + TN - 1) / TN) * ((K + TK - 1) / TK));
-  WgradPlan pl{tiles, tiles, 0, 1};
-  auto splits_for = [&](int t) {
-    int sp = (256 + t - 1) / t;
-    sp = sp < 8 ? sp : 8;
-    while (sp > 1 && M / sp < 2048) --sp;
-    return sp;
-  };
-  if (tiles < 256) {
-    const int sp = splits_for(tiles);
-    if (sp > 1) pl = WgradPlan{0, 0, tiles, sp};
-  } else {
-    static const bool tail_split = [] {  // EMA_WGRAD_TAIL=0: no tail split (A/B)
-      const char* e = getenv("EMA_WGRAD_TAIL");
-      return !(e && e[0] == '0');
-    }();
-    const int tail = tiles % 256;
-    if (tail_split && tail > 0 && tail <= 128) {
-      int sp = 256 / tail;
-      sp = sp < 8 ? sp : 8;
-      while (sp > 1 && M / sp < 2048) --sp;
-      if (sp > 1) pl = WgradPlan{tiles - tail, tiles - tail, tail, sp};
+// so a grid that is not a multiple of the CUs ends in a partial round, and a
+// grid of fewer tiles than CUs (TP-sharded projections) leaves CUs idle.  The
+// tiles of the partial round (all tiles when there are fewer than CUs) are
+// split over the tokens s ways, s picked by a cost model: rounds of tile
+// pieces, ceil(t s / CUs) / s tile-times, plus the fp32 partials' round trip
+// (t s blocks of 256 KB written and read back by the ordered reduce, ~5 TB/s)
+// and ~5 us of ring fill / epilogue per round; a split must win by 5 %.
+// At least 2048 tokens per split, at most 4 x CUs pieces (workspace bound).
+// E.g. the 7B TP8 shards: qkv / fc2 (96 tiles) 2 ways (was 3: 288 pieces =
+// two rounds), fc1 (176 tiles) unsplit (was 2: 352 pieces, two rounds of
+// half tiles plus the partials' traffic).
+namespace {
+int best_split(int t, int64_t M, int ncu) {
+  if (t <= 0) return 1;
+  const double tile_us = 2.0 * TN * TK * (double)M / (1.3e15 / ncu) * 1e6;
+  // per round: the pieces' compute + ~5 us of ring fill / epilogue
+  int best = 1;
+  double best_c = ((t + ncu - 1) / ncu) * (tile_us + 5.0);
+  for (int sp = 2; sp <= 16; ++sp) {
+    if (M / sp < 2048 || t * sp > 4 * ncu) break;
+    const int rounds = (t * sp + ncu - 1) / ncu;
+    const double c = rounds * (tile_us / sp + 5.0) +
+                     (double)t * sp * TN * TK * 4.0 * 2.0 / 5e12 * 1e6 + 3.0;
+    if (c < best_c * 0.95) {  // a split must win clearly (reduce launch, partial traffic)
+      best_c = c;
+      best = sp;
     }
   }
+  return best;
+}
+}  // namespace
+
+WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K) {
+  const int tiles = (int)(((N + TN - 1) / TN) * ((K + TK - 1) / TK));
+  const int ncu = 256;  // the plan must not depend on the device queried (host tests)
+  static const bool tail_split = [] {  // EMA_WGRAD_TAIL=0: no split (A/B)
+    const char* e = getenv("EMA_WGRAD_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  WgradPlan pl{tiles, tiles, 0, 1};
+  if (!tail_split) return pl;
+  const int tail = tiles < ncu ? tiles : tiles % ncu;
+  const int sp = best_split(tail, M, ncu);
+  if (sp > 1) pl = WgradPlan{tiles - tail, tiles - tail, tail, sp};
   return pl;
 }
 
@@ -851,18 +714,18 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   } else
   if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (accumulate) launch<bf16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<bf16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     } else if (dt == DT_F16) {
-      if (accumulate) launch<fp16, true, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<fp16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      else launch<fp16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
     }
   }
   if (split) {
     if (dt == DT_BF16)
-      launch<bf16, false, 0, 5>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<bf16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     else if (dt == DT_F16)
-      launch<fp16, false, 0, 5>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<fp16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
                        ws, g, iN, iK, tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK),
                        pl.tail_lin0, pl.tail_tiles,

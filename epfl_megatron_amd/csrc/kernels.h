@@ -236,13 +236,11 @@ struct WgradPlan {
   int main_tiles, tail_lin0, tail_tiles, nsplit;
 };
 bool wgrad_supported(int64_t M, int64_t N, int64_t K);
-void wgrad_set_variant(int v);  // 4: persistent 4-wave kernel (default), 8: 8-wave ping-pong
+void wgrad_set_variant(int v);  // 8: 8-wave ping-pong (default), 4: persistent 4-wave kernel
 WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K);
 int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
                 bool accumulate, int dt, hipStream_t s, float* ws = nullptr);
-void wgrad_gemm_ablation(const void* dy, const void* x, float* g, int64_t M, int64_t N,
-                         int64_t K, int mode, hipStream_t s);
 // ---- gemm_nt.hip: C[M,N] = A[M,K] B[N,K]^T (forward / dgrad), GLU epilogues --
 // Bench-only GEMM experiments (gemm_lab.hip): C = A B^T bf16, variant 0 =
 // production LDS layout, 1 = linear-source padded layout.

@@ -214,7 +214,9 @@ class Work:
                 raise CommRaceError(
                     f"{self._key}: buffer written while the collective was in flight "
                     f"(between launch and wait)")
-            self._run()
+            r = self._run()
+            if r is not None and hasattr(r, "wait"):
+                r.wait()  # stream-ordered work (loopback stream, p2p requests)
         elif self._work is not None:
             self._work.wait()
         if self._start is not None:
@@ -223,6 +225,43 @@ class Work:
             _PENDING_EVENTS.append((self._key, self._start, end))
         elif self._t0 is not None:
             _add_ms(self._key, (time.perf_counter() - self._t0) * 1e3)
+
+
+class _StreamWork:
+    """Handle of loopback work queued on the loopback stream (the stand-in for
+    RCCL's own stream): ``wait()`` orders the current stream behind it."""
+
+    __slots__ = ("_ev",)
+
+    def __init__(self, ev):
+        self._ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self._ev)
+
+
+_LOOP_STREAMS = {}
+
+
+def _loop_async(fn, tensors):
+    """Run a loopback collective's copies the way RCCL runs a collective: on a
+    stream of its own that first waits for the work already queued on the
+    current stream, overlapping whatever the caller queues next."""
+    if not tensors[0].is_cuda:
+        fn()
+        return None
+    cur = torch.cuda.current_stream()
+    s = _LOOP_STREAMS.get(cur.device)
+    if s is None:
+        s = _LOOP_STREAMS[cur.device] = torch.cuda.Stream(device=cur.device)
+    s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        fn()
+    for t in tensors:
+        t.record_stream(s)
+    ev = torch.cuda.Event()
+    ev.record(s)
+    return _StreamWork(ev)
 
 
 def _host_t0(t):
@@ -291,7 +330,8 @@ def reduce_scatter_into(output, inp, group=None, async_op=False, op="sum"):
         def loop(a):
             own = src.view(n, *output.shape)[0]
             if output.data_ptr() != own.data_ptr():
-                output.copy_(own)
+                return _loop_async(lambda: output.copy_(own), [output, src])
+            return None
         return _issue("reduce_scatter", group, src, src, loop, async_op)
     return _issue("reduce_scatter", group, src, src,
                   lambda a: dist.reduce_scatter_tensor(output, src, op=rop, group=group,
@@ -308,12 +348,16 @@ def all_gather_into(output, inp, group=None, async_op=False):
             # every simulated peer's slot gets this rank's shard: the output is
             # fully written each call (as a real all-gather writes it), so no
             # stale / non-finite bytes of a recycled allocation reach the loss
-            # (ADVICE r4), and the proxy's write traffic matches a real rank's
+            # (ADVICE r4); the copies run on the loopback stream, overlapping
+            # compute as RCCL's would, with a real rank's write traffic
             rows = output.view(n, -1)
             flat = src.reshape(1, -1)
-            if rows[0].data_ptr() != src.data_ptr():
-                rows[0:1].copy_(flat)
-            rows[1:].copy_(flat.expand(n - 1, -1))
+
+            def fill():
+                if rows[0].data_ptr() != src.data_ptr():
+                    rows[0:1].copy_(flat)
+                rows[1:].copy_(flat.expand(n - 1, -1))
+            return _loop_async(fill, [output, src])
         return _issue("all_gather", group, output, src, loop, async_op)
     xg = _XGMI.get(id(group))
     if xg is not None and xg.gather_eligible(output, src):

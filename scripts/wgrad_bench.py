@@ -65,33 +65,6 @@ def main():
 
 
 
-def ablation(modes=(0, 1, 2)):
-    """Time ablation/variant builds on fc1: mode % 10 = 1 no epilogue, 2 no global
-    loads; mode // 10 = schedule variant.  Checks each variant's numerics first."""
-    C = ext()
-    M, N, K = 16384, 22016, 4096
-    if os.environ.get("WG_SHAPE"):  # "N,K" (default: the 7B fc1 wgrad)
-        N, K = (int(v) for v in os.environ["WG_SHAPE"].split(","))
-    print(f"ablation shape M={M} N={N} K={K}", flush=True)
-    dY = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) - 0.5
-    X = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) - 0.5
-    G = torch.zeros(N, K, device="cuda", dtype=torch.float32)
-    for mode in modes:
-        if mode % 10 in (0, 3):
-            m, n, k = 1024, 768, 512
-            a = torch.randn(m, n, device="cuda", dtype=torch.bfloat16)
-            b = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
-            g = torch.randn(n, k, device="cuda")
-            ref = g + a.float().t() @ b.float()
-            C.wgrad_gemm_ablation(a, b, g, mode)
-            print(f"variant {mode} max err {(g - ref).abs().max().item():.3e}", flush=True)
-    fl = 2.0 * M * N * K
-    for rnd in range(2):
-        for mode in modes:
-            t = _time(lambda: C.wgrad_gemm_ablation(dY, X, G, mode))
-            print(f"ablation round {rnd} mode {mode}: {fl / t / 1e12:.1f} TF/s", flush=True)
-
-
 def variants(rounds=3):
     """Interleaved A/B (one process, CDNA guide rule 24) of the persistent 4-wave
     kernel, the 8-wave ping-pong kernel and hipBLASLt on the 7B wgrad shapes."""
@@ -122,8 +95,5 @@ def variants(rounds=3):
 if __name__ == "__main__":
     if "--variants" in sys.argv:
         variants()
-    elif "--ablation" in sys.argv:
-        i = sys.argv.index("--ablation")
-        ablation(tuple(int(v) for v in sys.argv[i + 1:]) or (0, 1, 2))
     else:
         main()

@@ -343,6 +343,19 @@ def test_flash_attention_falcon_shapes(nq, nkv):
     _attn_case(1, 320, nq, nkv, 64, torch.bfloat16, True, seed=nq)
 
 
+@pytest.mark.parametrize("b,s,nq,nkv,causal", [
+    (4, 1024, 32, 32, True),   # Llama-2-7B training shape: 512 blocks of 256 rows
+    (4, 1024, 32, 32, False),
+    (2, 2048, 32, 8, True),    # GQA at seq 2k
+    (1, 4000, 64, 64, True),   # partial last tile, 16 x 64 blocks
+])
+def test_flash_attention_8wave(b, s, nq, nkv, causal):
+    """Grids large enough for the 8-wave forward (staggered two-phase tile
+    loop by default, flash_attn_fwd.hip)."""
+    assert (s + 255) // 256 * nq * b >= 512  # flash_attn_waves() picks 8
+    _attn_case(b, s, nq, nkv, 128, torch.bfloat16, causal, seed=s + nkv)
+
+
 def test_flash_attention_running_max_jump():
     """Online-softmax rescale branch forced: one key row aligned with one query
     row so that row's running max jumps by a large margin at a late tile
@@ -685,15 +698,17 @@ def test_wgrad_gemm_variants(variant, M, N, K):
 
 
 def test_wgrad_plan():
-    """Split-K planning: small grids split every tile, a partial last round of
-    <= 128 tiles splits only the tail (7B fc1: 1376 tiles = 5 rounds + 96)."""
+    """Split-K planning (cost model): small grids split every tile, a partial
+    last round splits only its tiles (7B fc1: 1376 tiles = 5 rounds + 96)."""
     C = _ext()
     assert list(C.wgrad_plan(16384, 22016, 4096)) == [1280, 1280, 96, 2]
     assert list(C.wgrad_plan(16384, 12288, 4096)) == [768, 768, 0, 1]  # 3 full rounds
     assert list(C.wgrad_plan(16384, 4352, 4096)) == [256, 256, 16, 8]
     assert list(C.wgrad_plan(16384, 1536, 512)) == [0, 0, 12, 8]
     assert list(C.wgrad_plan(1024, 768, 512)) == [6, 6, 0, 1]  # too few tokens to split
-    assert list(C.wgrad_plan(16384, 2752, 4096)) == [0, 0, 176, 2]  # ragged: 11 x 16 tiles
+    # ragged 11 x 16 tiles: 2 x 176 pieces would take two rounds -> unsplit
+    assert list(C.wgrad_plan(16384, 2752, 4096)) == [176, 176, 0, 1]
+    assert list(C.wgrad_plan(16384, 1536, 4096)) == [0, 0, 96, 2]  # 2 x 96 in one round
 
 
 def test_lt_gemm_layouts():
