@@ -44,19 +44,7 @@ namespace {
 typedef __attribute__((ext_vector_type(2))) float f2;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
-// STAG (8 waves only): the two waves of a SIMD run half a tile apart.  Each
-// tile is two phases with a barrier after each, A = QK^T + V^T reads + online
-// softmax, B = PV; waves 4..7 enter the loop one barrier late, so on every
-// SIMD one wave's softmax VALU and QK^T run beside the other's PV MFMAs
-// instead of both waves hitting the same pipe at once (MFMA busy 23 % in the
-// lockstep form, profiles/r4aa_pmc_fa.txt).  Every wave issues its own DMA
-// pieces of tile t+2 at the start of its A(t) and retires them (counted
-// vmcnt) in time for the barrier in front of the first phase that reads tile
-// t+2: the end of B(t+1) for waves 0..3, the end of A(t+1) for waves 4..7.
-// WAR on the 3-slot ring: tile t+2 reuses tile t-1's slot, whose reads both
-// groups retired (lds_wait at the end of every A phase) before the barriers
-// the issue points follow.
-template <typename T, int HD, bool CAUSAL, int WAVES, bool STAG = false>
+template <typename T, int HD, bool CAUSAL, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnParams p) {
   typedef typename MT<T>::x8 x8;
   typedef typename MT<T>::x4 x4;
@@ -170,151 +158,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     trb[x] = RG * x + 64 * (4 * h + tq) + 16 * ((2 * ((lane >> 4) & 1) + (tp >> 1)) ^ ((h + 2 * x) & 3)) +
              8 * (tp & 1);
   }
-  // mask + online softmax of one 64-key tile (scores in place become P),
-  // running max / sum and the O rescale
-  auto fwd_softmax = [&](f32x16& s0, f32x16& s1, const int n0) {
-    // (causal: the key-count bound only binds when the diagonal offset
-    // reaches past sk, i.e. a context-parallel pair run with coff = sk)
-    const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax || n0 + KT > p.sk)
-                                  : (n0 + KT > p.sk);
-    if (need_mask) {
-      // element i of s0 is key n0 + acc_row(i, h), of s1 that + 32: with
-      // rc = acc_row(i, 0) the tests are rc <= hi and rc >= lo, one compare
-      // and one select per element (lo only under a document mask)
-      int hi = p.sk - 1 - n0 - 4 * h;
-      if (CAUSAL) hi = min(hi, qrow + off - n0 - 4 * h);
-      if (CAUSAL && p.doc_start) {
-        const int lo = ds_row - n0 - 4 * h;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rc = (i & 3) + 8 * (i >> 2);
-          if (rc > hi || rc < lo) s0[i] = -INFINITY;
-          if (rc + 32 > hi || rc + 32 < lo) s1[i] = -INFINITY;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rc = (i & 3) + 8 * (i >> 2);
-          if (rc > hi) s0[i] = -INFINITY;
-          if (rc + 32 > hi) s1[i] = -INFINITY;
-        }
-      }
-    }
-    // row max: 16 three-input max, the lane pair (l, l ^ 32) combined by one
-    // permlane32 swap (no LDS round trip)
-    float mt = fmaxf(s0[0], s1[0]);
-#pragma unroll
-    for (int i = 1; i < 16; ++i) mt = fmaxf(fmaxf(mt, s0[i]), s1[i]);
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt),
-                                                       false, false);
-      mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
-    }
-    const float m_new = fmaxf(m_i, mt);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
-    // p = exp2(s * scale * log2e - m): packed fma for the argument, packed
-    // adds for the row sum
-    const f2 sc2 = {sl2, sl2}, mm2 = {-m_use, -m_use};
-    f2 rs2 = {0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      f2 a = __builtin_elementwise_fma(f2{s0[i], s0[i + 1]}, sc2, mm2);
-      f2 b = __builtin_elementwise_fma(f2{s1[i], s1[i + 1]}, sc2, mm2);
-      a[0] = __builtin_amdgcn_exp2f(a[0]);
-      a[1] = __builtin_amdgcn_exp2f(a[1]);
-      b[0] = __builtin_amdgcn_exp2f(b[0]);
-      b[1] = __builtin_amdgcn_exp2f(b[1]);
-      s0[i] = a[0]; s0[i + 1] = a[1];
-      s1[i] = b[0]; s1[i + 1] = b[1];
-      rs2 += a;
-      rs2 += b;
-    }
-    float rsum = rs2[0] + rs2[1];
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(rsum),
-                                                       __float_as_uint(rsum), false, false);
-      rsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-    }
-    l_i = l_i * alpha + rsum;
-    m_i = m_new;
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
-    }
-  };
   __syncthreads();  // vmcnt(0) + barrier: tile 0 (and 1) landed
   if (p.stamps) st1 = fa::wall_stamp();
 
-  if constexpr (STAG) {
-    static_assert(WAVES == 8 && NB == 3, "the staggered loop is the 8-wave, 3-slot form");
-    const int grp = wave >> 2;
-    x4 vf[2][2][DT][2];
-    f32x16 s0, s1;
-    if (grp == 1) {
-      __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (MICROARCH, two waves per SIMD, 4)
-      __builtin_amdgcn_s_barrier();   // enter one phase late
-    }
-    for (int t = t0; t < ntiles; ++t) {
-      const bool act = t < wtiles && t >= wt0;
-      // ---- phase A(t): own DMA of tile t+2, QK^T, V^T reads, softmax
-      if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
-      if (act) {
-        const int n0 = t * KT;
-        const char* kl = lds + (t % NB) * 2 * TB;
-        const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
-        const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s0[i] = s1[i] = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int ko = rowb[kk & 1] + 512 * (kk >> 1);
-          const x8 ka0 = *reinterpret_cast<const x8*>(kl + ko);
-          const x8 ka1 = *reinterpret_cast<const x8*>(kl + 4 * RG + ko);
-          s0 = MT<T>::mfma(ka0, qf[kk], s0);
-          s1 = MT<T>::mfma(ka1, qf[kk], s1);
-        }
-        static_for<2>([&](auto subc) {
-          static_for<2>([&](auto scc) {
-            static_for<DT>([&](auto dcc) {
-              constexpr int vo = TB + decltype(subc)::value * 4 * RG + decltype(scc)::value * 2 * RG +
-                                 512 * decltype(dcc)::value;
-              vf[subc][scc][dcc][0] = tr_read_imm<vo, T>(trv0);
-              vf[subc][scc][dcc][1] = tr_read_imm<vo, T>(trv1);
-            });
-          });
-        });
-        fwd_softmax(s0, s1, n0);
-      }
-      lds_wait();  // this tile's reads retired before the barrier (slot reuse)
-      if (grp == 1) {
-        if (t + NB - 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      // ---- phase B(t): PV
-      if (act) {
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-          for (int sc = 0; sc < 2; ++sc) {
-            const x8 pf = acc_frag<T>(sub == 0 ? s0 : s1, sc);
-#pragma unroll
-            for (int dc = 0; dc < DT; ++dc)
-              o[dc] = MT<T>::mfma(join<T>(vf[sub][sc][dc][0], vf[sub][sc][dc][1]), pf, o[dc]);
-          }
-      }
-      if (grp == 0) {
-        if (t + NB - 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the barrier count
-    __builtin_amdgcn_s_setprio(0);
-  } else {
   for (int t = t0; t < ntiles; ++t) {
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
     // retired before the barrier that ended tile t-1
@@ -348,7 +194,77 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
           });
         });
       });
-      fwd_softmax(s0, s1, n0);
+      // (causal: the key-count bound only binds when the diagonal offset
+      // reaches past sk, i.e. a context-parallel pair run with coff = sk)
+      const bool need_mask = CAUSAL ? (n0 + KT - 1 > m0 + off || n0 < ds_wmax || n0 + KT > p.sk)
+                                    : (n0 + KT > p.sk);
+      if (need_mask) {
+        // element i of s0 is key n0 + acc_row(i, h), of s1 that + 32: with
+        // rc = acc_row(i, 0) the tests are rc <= hi and rc >= lo, one compare
+        // and one select per element (lo only under a document mask)
+        int hi = p.sk - 1 - n0 - 4 * h;
+        if (CAUSAL) hi = min(hi, qrow + off - n0 - 4 * h);
+        if (CAUSAL && p.doc_start) {
+          const int lo = ds_row - n0 - 4 * h;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int rc = (i & 3) + 8 * (i >> 2);
+            if (rc > hi || rc < lo) s0[i] = -INFINITY;
+            if (rc + 32 > hi || rc + 32 < lo) s1[i] = -INFINITY;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int rc = (i & 3) + 8 * (i >> 2);
+            if (rc > hi) s0[i] = -INFINITY;
+            if (rc + 32 > hi) s1[i] = -INFINITY;
+          }
+        }
+      }
+      // row max: 16 three-input max, the lane pair (l, l ^ 32) combined by one
+      // permlane32 swap (no LDS round trip)
+      float mt = fmaxf(s0[0], s1[0]);
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mt = fmaxf(fmaxf(mt, s0[i]), s1[i]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt),
+                                                         false, false);
+        mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+      }
+      const float m_new = fmaxf(m_i, mt);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
+      // p = exp2(s * scale * log2e - m): packed fma for the argument, packed
+      // adds for the row sum
+      const f2 sc2 = {sl2, sl2}, mm2 = {-m_use, -m_use};
+      f2 rs2 = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        f2 a = __builtin_elementwise_fma(f2{s0[i], s0[i + 1]}, sc2, mm2);
+        f2 b = __builtin_elementwise_fma(f2{s1[i], s1[i + 1]}, sc2, mm2);
+        a[0] = __builtin_amdgcn_exp2f(a[0]);
+        a[1] = __builtin_amdgcn_exp2f(a[1]);
+        b[0] = __builtin_amdgcn_exp2f(b[0]);
+        b[1] = __builtin_amdgcn_exp2f(b[1]);
+        s0[i] = a[0]; s0[i + 1] = a[1];
+        s1[i] = b[0]; s1[i + 1] = b[1];
+        rs2 += a;
+        rs2 += b;
+      }
+      float rsum = rs2[0] + rs2[1];
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(rsum),
+                                                         __float_as_uint(rsum), false, false);
+        rsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+      }
+      l_i = l_i * alpha + rsum;
+      m_i = m_new;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      }
       lds_wait();
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -369,7 +285,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     }
   }
 
-  }
   if (p.stamps) st2 = fa::wall_stamp();
   if (qrow < p.sq) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
@@ -430,29 +345,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   }
 }
 
-// EMA_FA_STAGGER=0 selects the lockstep 8-wave loop (A/B against the
-// staggered one; scripts/fa_bench.py)
-bool fwd_stagger() {
-  static const bool on = [] {
-    const char* e = getenv("EMA_FA_STAGGER");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
-
 template <typename T, int HD, int WAVES>
 void launch_fwd(const AttnParams& p, hipStream_t s) {
   const int bmw = 32 * WAVES;
   dim3 grid(((p.sq + bmw - 1) / bmw) * p.nq * p.b);
-  if constexpr (WAVES == 8) {
-    if (fwd_stagger()) {
-      if (p.causal)
-        hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES, true>), grid, dim3(64 * WAVES), 0, s, p);
-      else
-        hipLaunchKernelGGL((fa_fwd_k<T, HD, false, WAVES, true>), grid, dim3(64 * WAVES), 0, s, p);
-      return;
-    }
-  }
   if (p.causal)
     hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
   else

@@ -4,8 +4,8 @@
 
 Default shapes: the Llama-2-7B training shape (8 x 1024, 32 heads) and the
 seq-4096 one.  Per shape: median over 20 timed forward calls and over 10
-forward+backward pairs (backward time = pair - forward).  Set EMA_FA_STAGGER /
-EMA_FA_WAVES in the environment to A/B the forward schedules.
+forward+backward pairs (backward time = pair - forward).  EMA_FA_WAVES=4|8
+forces the forward / dQ grid form.
 """
 import os
 import statistics
@@ -49,8 +49,7 @@ def run(b, s, nq, nkv, hd):
         q.grad = k.grad = v.grad = None
     f, bw = statistics.median(tf), statistics.median(tb)
     print(f"b={b} s={s} nq={nq} nkv={nkv} hd={hd}: fwd {f * 1e3:.1f} us ({fl / f / 1e9:.0f} TF/s)  "
-          f"bwd {bw * 1e3:.1f} us ({2.5 * fl / bw / 1e9:.0f} TF/s)  "
-          f"[stagger={os.environ.get('EMA_FA_STAGGER', 'default')}]", flush=True)
+          f"bwd {bw * 1e3:.1f} us ({2.5 * fl / bw / 1e9:.0f} TF/s)", flush=True)
 
 
 def main():

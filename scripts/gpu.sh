@@ -17,7 +17,7 @@
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
-#   fa         scripts/fa_bench.py (staggered forward, then EMA_FA_STAGGER=0)
+#   fa         scripts/fa_bench.py
 #   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
 #   px70       bench.py --proxy llama70b-tp8
 #   pmc_lab    rocprofv3 --pmc passes over scripts/gemm_lab.py (one pass per run)
@@ -70,9 +70,7 @@ for step in "$@"; do
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
-    fa) run fa 400 python -u scripts/fa_bench.py
-        EMA_FA_STAGGER=0 run fa0 300 python -u scripts/fa_bench.py
-        cat "gpurun_out/${TAG}_fa.log" "gpurun_out/${TAG}_fa0.log" ;;
+    fa) run fa 400 python -u scripts/fa_bench.py ;;
     px7) run px7 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     px70) run px70 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;
     pmc_lab)

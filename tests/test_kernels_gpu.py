@@ -350,8 +350,8 @@ def test_flash_attention_falcon_shapes(nq, nkv):
     (1, 4000, 64, 64, True),   # partial last tile, 16 x 64 blocks
 ])
 def test_flash_attention_8wave(b, s, nq, nkv, causal):
-    """Grids large enough for the 8-wave forward (staggered two-phase tile
-    loop by default, flash_attn_fwd.hip)."""
+    """Grids large enough for the 8-wave forward and dQ kernels (3-slot K/V
+    ring, flash_attn_fwd.hip / flash_attn_bwd.hip)."""
     assert (s + 255) // 256 * nq * b >= 512  # flash_attn_waves() picks 8
     _attn_case(b, s, nq, nkv, 128, torch.bfloat16, causal, seed=s + nkv)
 
