@@ -14,6 +14,7 @@
 #   bench      bench.py --steps 8 --warmup 2 (the headline config)
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
 #   profpx7    rocprofv3 kernel trace of the llama7b-tp8 proxy (profpx70: llama70b-tp8)
+#   ab         bench.py twice plain / twice with $AB_ENV, interleaved
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
@@ -67,6 +68,14 @@ for step in "$@"; do
     prof) prof prof 600 python3 -u bench.py --steps 2 --warmup 1 $BENCH_ARGS ;;
     profpx7) prof profpx7 600 python3 -u bench.py --proxy llama7b-tp8 --steps 2 --warmup 1 ;;
     profpx70) prof profpx70 900 python3 -u bench.py --proxy llama70b-tp8 --steps 1 --warmup 1 ;;
+    ab)  # interleaved bench A/B: plain, then with $AB_ENV (e.g. AB_ENV="EMA_X=1"), twice
+      for i in 1 2; do
+        run "ab${i}a" 400 python -u bench.py --steps 6 --warmup 2 $BENCH_ARGS
+        run "ab${i}b" 400 env $AB_ENV python -u bench.py --steps 6 --warmup 2 $BENCH_ARGS
+      done
+      for f in gpurun_out/${TAG}_ab*.log; do
+        echo "$f $(grep -o '"value": [0-9.]*' "$f")"
+      done ;;
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
