@@ -18,6 +18,7 @@
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
+#   px7ab      the TP8 proxy plain, then with $AB_ENV
 #   fa         scripts/fa_bench.py
 #   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
 #   px70       bench.py --proxy llama70b-tp8
@@ -79,6 +80,9 @@ for step in "$@"; do
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
+    px7ab)  # TP8 proxy, plain then with $AB_ENV
+      run px7a 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2
+      run px7b 500 env $AB_ENV python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     fa) run fa 400 python -u scripts/fa_bench.py ;;
     px7) run px7 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     px70) run px70 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;
