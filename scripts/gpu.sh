@@ -15,6 +15,7 @@
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
 #   profpx7    rocprofv3 kernel trace of the llama7b-tp8 proxy (profpx70: llama70b-tp8)
 #   ab         bench.py twice plain / twice with $AB_ENV, interleaved
+#   ltre       scripts/lt_retune.py (torch.matmul's hipBLASLt pick vs the best solution)
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
@@ -77,6 +78,7 @@ for step in "$@"; do
       for f in gpurun_out/${TAG}_ab*.log; do
         echo "$f $(grep -o '"value": [0-9.]*' "$f")"
       done ;;
+    ltre) run ltre 500 python -u scripts/lt_retune.py ;;
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
