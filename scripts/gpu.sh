@@ -21,6 +21,7 @@
 #   wgrad      scripts/wgrad_ab.py (4-wave vs 8-wave wgrad vs hipBLASLt)
 #   px7ab      the TP8 proxy plain, then with $AB_ENV
 #   fa         scripts/fa_bench.py
+#   faab       scripts/fa_bench.py plain / with $AB_ENV, interleaved twice
 #   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
 #   px70       bench.py --proxy llama70b-tp8
 #   pmc_lab    rocprofv3 --pmc passes over scripts/gemm_lab.py (one pass per run)
@@ -86,8 +87,30 @@ for step in "$@"; do
       run px7a 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2
       run px7b 500 env $AB_ENV python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     fa) run fa 400 python -u scripts/fa_bench.py ;;
+    faab)  # FA timing plain, then with $AB_ENV, twice
+      for i in 1 2; do
+        run "fa${i}a" 300 python -u scripts/fa_bench.py
+        run "fa${i}b" 300 env $AB_ENV python -u scripts/fa_bench.py
+      done
+      grep -h "fwd" gpurun_out/${TAG}_fa?[ab].log ;;
     px7) run px7 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
     px70) run px70 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;
+    pmc_fa)  # FA forward counters, plain then with $AB_ENV (one pass per run)
+      export TMPDIR=/tmp
+      i=0
+      for ctr in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
+                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+        i=$((i + 1))
+        run "pmcfa${i}a" 60 rocprofv3 --pmc $ctr --output-format csv -d "gpurun_out/${TAG}_pmcfa_a${i}" -o pmc -- \
+          python3 -u scripts/fa_pmc_one.py
+        export $AB_ENV
+        run "pmcfa${i}b" 60 rocprofv3 --pmc $ctr --output-format csv -d "gpurun_out/${TAG}_pmcfa_b${i}" -o pmc -- \
+          python3 -u scripts/fa_pmc_one.py
+        unset ${AB_ENV%%=*}
+      done
+      python scripts/pmc_table.py gpurun_out/${TAG}_pmcfa_a* > "gpurun_out/${TAG}_pmcfa_a.txt" 2>&1
+      python scripts/pmc_table.py gpurun_out/${TAG}_pmcfa_b* > "gpurun_out/${TAG}_pmcfa_b.txt" 2>&1
+      grep -A2 "fa_fwd" "gpurun_out/${TAG}_pmcfa_a.txt" "gpurun_out/${TAG}_pmcfa_b.txt" | cut -c1-600 ;;
     pmc_lab)
       export TMPDIR=/tmp
       i=0
