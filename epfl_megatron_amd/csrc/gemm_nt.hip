@@ -1029,6 +1029,7 @@ int group_m(int ntm, int ntn) {
 // 1.05x; plain products 0.93-0.99x hipBLASLt, so those stay on hipBLASLt
 // in-model unless a row map needs this kernel).
 // EMA_GEMM_NT=<v> or gemm_nt_set_variant(v) forces one variant everywhere
+// (EMA_GEMM_NT_STORE=<v>: the plain / row-mapped products only)
 // (A/B in one process); gemm_nt_set_variant(0) restores the defaults.
 int g_var[3] = {6, 6, 6};  // [EPI_STORE, EPI_GLU, EPI_DGLU]
 int parse_variant(int v) { return (v == 4 || v == 5 || v == 6 || v == 8) ? v : 0; }
@@ -1036,6 +1037,9 @@ const int g_env_variant = [] {
   const char* e = getenv("EMA_GEMM_NT");
   const int v = e ? parse_variant(atoi(e)) : 0;
   if (v) g_var[0] = g_var[1] = g_var[2] = v;
+  const char* es = getenv("EMA_GEMM_NT_STORE");  // plain / row-mapped products only
+  const int vs = es ? parse_variant(atoi(es)) : 0;
+  if (vs) g_var[0] = vs;
   return v;
 }();
 

@@ -26,6 +26,7 @@ Two debug/observability aids live here:
   gradients; the CPU tests run with the checker on.
 """
 import os
+import weakref
 import time
 from collections import OrderedDict
 
@@ -61,9 +62,10 @@ def set_loopback(group, world):
     """Make ``group`` (a real 1-rank group) stand for ``world`` ranks: its
     collectives are accounted with a real rank's bytes but move (almost) none,
     so the proxy's timed step holds no emulation kernels a real rank would not
-    run: all-gather writes only this rank's own shard into
-    its slot (the other ranks' slots are zero-filled once per buffer and then
-    left as they are — finite stand-ins for the bytes xGMI would deliver),
+    run: all-gather writes this rank's shard into its
+    slot, and into the other ranks' slots too -- every call for a fresh
+    output, once per range for a persistent scratch buffer (finite stand-ins
+    for the bytes xGMI would deliver, never recycled garbage),
     reduce-scatter writes this rank's own chunk (no reduction), all-reduce /
     broadcast are identities.  Used by the one-GPU per-rank proxies of the TP
     configurations; the numbers they train on are not a real TP run's."""
@@ -241,13 +243,34 @@ class _StreamWork:
 
 
 _LOOP_STREAMS = {}
+# EMA_LOOPBACK_STREAM=1: loopback copies on a stream of their own, as RCCL's
+# kernels run.  Off by default: the copies are CU kernels (RCCL's run on a few
+# CUs), and beside the persistent GEMMs they cost both TP proxies 4 %
+# (profiles/r5x_loopback_stream_ab.txt).
+_LOOP_SIDE_STREAM = os.environ.get("EMA_LOOPBACK_STREAM", "0") == "1"
+# Simulated peers' slots of a loopback all-gather into a persistent scratch
+# buffer (parallel/buffers.py) are written once per (buffer, range): they then
+# hold finite activations for good, and the per-call traffic is this rank's
+# own slot, as the proxy's compute-only accounting assumes.  Any other output
+# (a fresh allocation that may hold recycled bytes) is fully written each call.
+_LOOP_FILLED = {}  # id(scratch buffer) -> filled (offset, numel); dropped with the buffer
+
+
+def _scratch_owner(t):
+    """The live GlobalMemoryBuffer tensor holding ``t`` (None: not scratch)."""
+    from .buffers import get_global_memory_buffer
+    ptr = t.untyped_storage().data_ptr()
+    for buf in get_global_memory_buffer()._buffers.values():
+        if buf.untyped_storage().data_ptr() == ptr:
+            return buf
+    return None
 
 
 def _loop_async(fn, tensors):
     """Run a loopback collective's copies the way RCCL runs a collective: on a
     stream of its own that first waits for the work already queued on the
     current stream, overlapping whatever the caller queues next."""
-    if not tensors[0].is_cuda:
+    if not tensors[0].is_cuda or not _LOOP_SIDE_STREAM:
         fn()
         return None
     cur = torch.cuda.current_stream()
@@ -352,11 +375,20 @@ def all_gather_into(output, inp, group=None, async_op=False):
             # compute as RCCL's would, with a real rank's write traffic
             rows = output.view(n, -1)
             flat = src.reshape(1, -1)
+            owner = _scratch_owner(output)
+            key = (output.storage_offset(), output.numel())
+            if owner is not None and id(owner) not in _LOOP_FILLED:
+                _LOOP_FILLED[id(owner)] = set()
+                weakref.finalize(owner, _LOOP_FILLED.pop, id(owner), None)
+            peers = owner is None or key not in _LOOP_FILLED[id(owner)]
 
             def fill():
                 if rows[0].data_ptr() != src.data_ptr():
                     rows[0:1].copy_(flat)
-                rows[1:].copy_(flat.expand(n - 1, -1))
+                if peers:
+                    rows[1:].copy_(flat.expand(n - 1, -1))
+            if owner is not None:
+                _LOOP_FILLED[id(owner)].add(key)
             return _loop_async(fill, [output, src])
         return _issue("all_gather", group, output, src, loop, async_op)
     xg = _XGMI.get(id(group))

@@ -83,6 +83,9 @@ for step in "$@"; do
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
+    px70ab)  # 70B TP8 proxy, plain then with $AB_ENV
+      run px70a 700 python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1
+      run px70b 700 env $AB_ENV python -u bench.py --proxy llama70b-tp8 --steps 3 --warmup 1 ;;
     px7ab)  # TP8 proxy, plain then with $AB_ENV
       run px7a 500 python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2
       run px7b 500 env $AB_ENV python -u bench.py --proxy llama7b-tp8 --steps 6 --warmup 2 ;;
