@@ -1044,8 +1044,12 @@ at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::T
   const ema::RowMap cm = row_map(c_map, M, c.size(0), "gemm_nt c_map");
   TORCH_CHECK(ema::gemm_nt_supported(M, N, K, a.stride(0), b.stride(0), c.stride(0)),
               "gemm_nt: unsupported shape (K % 32, N % 8)");
+  // few-tile products split K over fp32 partials (caching allocator, ordered reduce)
+  const int64_t wsf = ema::gemm_nt_workspace_floats(M, N, K);
+  at::Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, a.options().dtype(at::kFloat));
   ema::gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0), b.stride(0),
-               c.stride(0), dt, cur_stream(), am, cm);
+               c.stride(0), dt, cur_stream(), am, cm, wsf > 0 ? ws.data_ptr<float>() : nullptr);
   return c;
 }
 

@@ -122,6 +122,8 @@ struct NtArgs {
   int ntm, ntn, gm;
   bool wave4_ok;      // 32-bit per-lane DMA offsets fit (the 4-wave kernel)
   RowMap am, cm;      // row-group remap of A rows (loads) and C rows (stores)
+  int ksplit;         // EPI_STORE, persistent kernel: K split this many ways
+  float* ws;          // ... fp32 partial tiles [ksplit][tiles][256][256] (ksplit > 1)
 };
 
 // logical row q -> physical row (RowMap in kernels.h); q < 2^31
@@ -856,11 +858,16 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int ntiles = p.ntm * p.ntn;
+  // split-K (EPI_STORE, few tiles): item = (split, tile), split-major; each
+  // item runs nt = K / BK2 / ksplit K-steps from K-step ks * nt and stores
+  // an fp32 partial tile, summed by gemm_nt_split_reduce_k
+  const int ksplit = EPI == EPI_STORE ? p.ksplit : 1;
+  const int nitems = ntiles * ksplit;
   const int G = gridDim.x, bid = blockIdx.x;
-  if (bid >= ntiles) return;
-  const int nmine = (ntiles - 1 - bid) / G + 1;
+  if (bid >= nitems) return;
+  const int nmine = (nitems - 1 - bid) / G + 1;
   const int M = p.M, N = p.N;
-  const int nt = p.K / BK2;  // >= 2 (host-checked)
+  const int nt = p.K / BK2 / ksplit;  // >= 2 (host-checked)
 
   // per-lane DMA byte offsets inside a tile (fixed for the whole kernel);
   // piece i of the 4 waves = 32 consecutive rows (+1-3 %, profiles/r4h_gemm_ablation.txt)
@@ -881,10 +888,12 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   }
   // tile i of this workgroup -> (m0, n0): n0 = first output column, or first
   // f (EPI_GLU: 128 per tile)
-  auto tile_org = [&](int i, int64_t& m0, int64_t& n0) {
-    const int base = i * G, rem = min(G, ntiles - base);
-    const int lin = base + xcd_remap(bid, rem);
-    const int2 tt = tile_of(lin, p.ntm, p.ntn, p.gm);
+  auto tile_org = [&](int i, int64_t& m0, int64_t& n0, int& ks, int& lt) {
+    const int base = i * G, rem = min(G, nitems - base);
+    const int item = base + xcd_remap(bid, rem);
+    ks = item / ntiles;
+    lt = item - ks * ntiles;
+    const int2 tt = tile_of(lt, p.ntm, p.ntn, p.gm);
     m0 = (int64_t)tt.x * TM;
     n0 = (int64_t)tt.y * (EPI == EPI_GLU ? TN / 2 : TN);
   };
@@ -892,18 +901,20 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
     int64_t m0 = 0, n0 = 0;
     int64_t na = 0, nb = 0;
-    int64_t am0 = 0;
+    int64_t am0 = 0, koff = 0;  // koff: bytes of K before this item's split
     if (i < nmine) {
-      tile_org(i, m0, n0);
+      int ks, lt;
+      tile_org(i, m0, n0, ks, lt);
+      koff = (int64_t)ks * nt * BK2 * (int64_t)sizeof(T);
       // a row map's groups hold whole 256-row tiles (host-checked): the tile's
       // physical rows are contiguous from map_row(m0)
       am0 = map_row(m0, p.am);
       const int64_t arows = p.am.rows == 0 ? M - m0 : min((int64_t)TM, (int64_t)M - m0);
-      na = arows * p.lda * (int64_t)sizeof(T);
-      nb = (int64_t)((EPI == EPI_GLU ? 2 * (int64_t)N : N) - n0) * p.ldb * (int64_t)sizeof(T);
+      na = arows * p.lda * (int64_t)sizeof(T) - koff;
+      nb = (int64_t)((EPI == EPI_GLU ? 2 * (int64_t)N : N) - n0) * p.ldb * (int64_t)sizeof(T) - koff;
     }
-    const char* a = reinterpret_cast<const char*>(p.a) + am0 * p.lda * (int64_t)sizeof(T);
-    const char* b = reinterpret_cast<const char*>(p.b) + n0 * p.ldb * (int64_t)sizeof(T);
+    const char* a = reinterpret_cast<const char*>(p.a) + am0 * p.lda * (int64_t)sizeof(T) + koff;
+    const char* b = reinterpret_cast<const char*>(p.b) + n0 * p.ldb * (int64_t)sizeof(T) + koff;
     ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, (int)min(na, (int64_t)0x7fffffff), 0x00020000);
     rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)min(nb, (int64_t)0x7fffffff), 0x00020000);
   };
@@ -994,14 +1005,65 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
     // K-steps are (or have been) landing in LDS
     fa::mfma_drain();
     int64_t m0, n0;
-    tile_org(i, m0, n0);
-    epilogue_regs<T, EPI, ACT>(p, acc, lane, m0 + 128 * wm, n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
+    int ks, lt;
+    tile_org(i, m0, n0, ks, lt);
+    if (EPI == EPI_STORE && ksplit > 1) {
+      // fp32 partial: the wave's 128 x 128 block of the dense 256 x 256 tile
+      float* w = p.ws + ((int64_t)ks * ntiles + lt) * (TM * TN) + (128 * wm + (lane & 15)) * TN +
+                 128 * wn + 4 * (lane >> 4);
+      static_for<8>([&](auto iic) {
+        constexpr int ii = decltype(iic)::value;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          __builtin_nontemporal_store(acc[ii][jj], reinterpret_cast<f32x4*>(w + 16 * ii * TN + 16 * jj));
+        __builtin_amdgcn_sched_barrier(0);  // one row group's accumulators in VGPRs at a time
+      });
+    } else {
+      epilogue_regs<T, EPI, ACT>(p, acc, lane, m0 + 128 * wm, n0 + (EPI == EPI_GLU ? 64 : 128) * wn);
+    }
     par ^= nt & 1;
     ra_c = ra_n;
     rb_c = rb_n;
     make_rsrc(i + 2, ra_n, rb_n);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// C[tile] = sum over the K splits of ws[split][tile] (fixed order), rounded
+// to T, stored through the C row map; 64 workgroups x 256 threads x 4 per tile
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_nt_split_reduce_k(NtArgs p) {
+  const int ntiles = p.ntm * p.ntn;
+  const int lt = blockIdx.x / 64, part = blockIdx.x % 64;
+  const int2 tt = tile_of(lt, p.ntm, p.ntn, p.gm);
+  const int e = (part * 256 + threadIdx.x) * 4;
+  const int row = e / TN, col = e % TN;
+  const int64_t m = (int64_t)tt.x * TM + row, n = (int64_t)tt.y * TN + col;
+  if (m >= p.M || n >= p.N) return;  // N % 8 == 0: a 4-column piece is all in or all out
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int ks = 0; ks < p.ksplit; ++ks)
+    acc += __builtin_nontemporal_load(
+        reinterpret_cast<const f32x4*>(p.ws + ((int64_t)ks * ntiles + lt) * (TM * TN) + e));
+  *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.c) + map_row(m, p.cm) * p.ldc + n) = pack4<T>(acc);
+}
+
+// K split of a plain / row-mapped product on the persistent kernel: products
+// of fewer than half a grid of tiles (TP-sharded narrow outputs: the 70B TP8
+// qkv pieces are 80 tiles, the dense dgrad pieces 64) split K so that about
+// one item per CU runs; at least 8 K-steps of 64 per item.  EMA_GEMM_NT_SPLITK=0
+// disables.
+int nt_ksplit(int tiles, int64_t K) {
+  static const bool on = [] {
+    const char* e = getenv("EMA_GEMM_NT_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  const int ncu = 256;  // plan independent of the device queried (host tests)
+  if (!on || tiles * 2 > ncu || K % BK2 != 0) return 1;
+  const int steps = (int)(K / BK2);
+  int best = 1;
+  for (int sp = 2; sp <= 8; ++sp)
+    if (tiles * sp <= ncu && steps % sp == 0 && steps / sp >= 8) best = sp;
+  return best;
 }
 
 int group_m(int ntm, int ntn) {
@@ -1069,8 +1131,14 @@ void launch_one(const NtArgs& p, hipStream_t s) {
     const int64_t a_extent = p.am.rows == 0 ? (int64_t)p.M : (int64_t)TM;  // rows one descriptor spans
     if (g_var[EPI] == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 && maps_ok &&
         a_extent * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
-      const int g = std::min(p.ntm * p.ntn, num_cus());
-      hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, p);
+      const int items = p.ntm * p.ntn * (EPI == EPI_STORE && p.ws ? p.ksplit : 1);
+      const int g = std::min(items, num_cus());
+      NtArgs q = p;
+      if (!(EPI == EPI_STORE && p.ws)) q.ksplit = 1;
+      hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, q);
+      if (EPI == EPI_STORE && q.ksplit > 1)
+        hipLaunchKernelGGL(gemm_nt_split_reduce_k<T>, dim3((unsigned)(p.ntm * p.ntn * 64)), dim3(256),
+                           0, s, q);
       return;
     }
   }
@@ -1118,10 +1186,22 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
          ((M + TM - 1) / TM) * ((N + TN / 2 - 1) / (TN / 2)) < ((int64_t)1 << 31);
 }
 
+int64_t gemm_nt_workspace_floats(int64_t M, int64_t N, int64_t K) {
+  if (g_var[EPI_STORE] != 6) return 0;
+  const int tiles = (int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
+  const int sp = nt_ksplit(tiles, K);
+  return sp > 1 ? (int64_t)sp * tiles * TM * TN : 0;
+}
+
 void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
-             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap, RowMap cmap) {
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap, RowMap cmap, float* ws) {
   NtArgs p{a, b, c, nullptr, nullptr, lda, ldb, ldc, 0, (int)M, (int)N, (int)K, 0, 0, 0, false,
-           amap, cmap};
+           amap, cmap, 1, nullptr};
+  if (ws) {
+    p.ksplit = nt_ksplit((int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN)), K);
+    p.ws = p.ksplit > 1 ? ws : nullptr;
+    if (!p.ws) p.ksplit = 1;
+  }
   launch_nt<EPI_STORE>(p, 0, dt, s);
 }
 
@@ -1129,14 +1209,14 @@ void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, in
                  int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s,
                  RowMap cmap) {
   NtArgs p{a, b, pre, y, nullptr, lda, ldb, 2 * F, F, (int)M, (int)F, (int)K, 0, 0, 0, false,
-           RowMap{}, cmap};
+           RowMap{}, cmap, 1, nullptr};
   launch_nt<EPI_GLU>(p, kind, dt, s);
 }
 
 void gemm_nt_dglu(const void* a, const void* b, const void* pre, void* dpre, int64_t M, int64_t F,
                   int64_t K, int64_t lda, int64_t ldb, int kind, int dt, hipStream_t s) {
   NtArgs p{a, b, dpre, nullptr, pre, lda, ldb, 2 * F, 0, (int)M, (int)F, (int)K, 0, 0, 0, false,
-           RowMap{}, RowMap{}};
+           RowMap{}, RowMap{}, 1, nullptr};
   launch_nt<EPI_DGLU>(p, kind, dt, s);
 }
 

@@ -256,7 +256,10 @@ struct RowMap {
   int64_t stride = 0, offset = 0;
 };
 void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
-             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap = {}, RowMap cmap = {});
+             int64_t ldb, int64_t ldc, int dt, hipStream_t s, RowMap amap = {}, RowMap cmap = {},
+             float* ws = nullptr);
+// fp32 workspace (floats) gemm_nt splits K into for few-tile products (0: none)
+int64_t gemm_nt_workspace_floats(int64_t M, int64_t N, int64_t K);
 // fc1 forward: b = W1 [2F, K]; writes pre [M, 2F] and y = x1 * act(x2) [M, F]
 // (rows of both outputs through cmap)
 void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,

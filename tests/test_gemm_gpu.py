@@ -252,6 +252,35 @@ def test_gemm_nt_row_maps(tp, c, R, N, K):
     assert y.view(tp, c, R, F)[:, 1:].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("tp,c,R,N,K", [
+    (1, 1, 1024, 1280, 8192),   # 20 tiles: K split 8 ways
+    (8, 2, 256, 1280, 8192),    # Llama-2-70B TP8 qkv piece (80 tiles at 512-row groups: 2 ways)
+    (8, 2, 256, 1000, 8192),    # ragged N
+    (8, 2, 256, 1024, 4096),    # dense-dgrad-like piece through a C map
+])
+def test_gemm_nt_split_k(tp, c, R, N, K):
+    """Few-tile products on the persistent kernel split K over fp32 partials
+    (gemm_nt_split_reduce_k, fixed order): A / C row maps, ragged N, and
+    bitwise-reproducible results."""
+    torch.manual_seed(6)
+    b = _rand(N, K, scale=K ** -0.5)
+    full = _rand(tp * c * R, K)
+    j = c - 1
+    amap = [R, c * R, j * R] if c > 1 else []
+    out = _ext().gemm_nt(full, b, a_map=amap, m=tp * R)
+    out2 = _ext().gemm_nt(full, b, a_map=amap, m=tp * R)
+    ref = full.view(tp, c, R, K)[:, j].reshape(tp * R, K).float() @ b.float().t()
+    assert out.shape == (tp * R, N) and _rel_err(out, ref) < 1e-2
+    assert torch.equal(out, out2)
+    if c > 1:
+        g = _rand(tp * R, K)
+        dst = torch.zeros(tp * c * R, N, device=DEV, dtype=torch.bfloat16)
+        _ext().gemm_nt(g, b, dst, c_map=[R, c * R, 0])
+        v = dst.view(tp, c, R, N)
+        assert _rel_err(v[:, 0].reshape(tp * R, N), g.float() @ b.float().t()) < 1e-2
+        assert v[:, 1:].abs().sum().item() == 0
+
+
 def test_gemm_nt_row_map_out_of_range_refused():
     a = _rand(256, 64)
     b = _rand(256, 64)
