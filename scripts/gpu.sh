@@ -25,6 +25,7 @@
 #   px7        bench.py --proxy llama7b-tp8 (one TP rank, simulated TP)
 #   px70       bench.py --proxy llama70b-tp8
 #   pmc_lab    rocprofv3 --pmc passes over scripts/gemm_lab.py (one pass per run)
+#   pmc_gemms  one rocprofv3 --pmc pass over the NT GEMM bench and the wgrad A/B
 # Extra bench.py arguments: BENCH_ARGS="..." in the environment.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -114,6 +115,16 @@ for step in "$@"; do
       python scripts/pmc_table.py gpurun_out/${TAG}_pmcfa_a* > "gpurun_out/${TAG}_pmcfa_a.txt" 2>&1
       python scripts/pmc_table.py gpurun_out/${TAG}_pmcfa_b* > "gpurun_out/${TAG}_pmcfa_b.txt" 2>&1
       grep -A2 "fa_fwd" "gpurun_out/${TAG}_pmcfa_a.txt" "gpurun_out/${TAG}_pmcfa_b.txt" | cut -c1-600 ;;
+    pmc_gemms)  # one PMC pass over the NT GEMM bench (variant 6) and the wgrad A/B
+      export TMPDIR=/tmp
+      CTR="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+      run pmcnt 120 rocprofv3 --pmc $CTR --output-format csv -d "gpurun_out/${TAG}_pmcnt" -o pmc -- \
+        python3 -u scripts/gemm_nt_bench.py --variants 6 --rounds 1 --iters 2
+      run pmcwg 120 rocprofv3 --pmc $CTR --output-format csv -d "gpurun_out/${TAG}_pmcwg" -o pmc -- \
+        python3 -u scripts/wgrad_ab.py
+      python scripts/pmc_table.py gpurun_out/${TAG}_pmcnt > "gpurun_out/${TAG}_pmcnt_table.txt" 2>&1
+      python scripts/pmc_table.py gpurun_out/${TAG}_pmcwg > "gpurun_out/${TAG}_pmcwg_table.txt" 2>&1
+      grep -h -A2 "wgrad\|gemm_nt6\|Cijk" gpurun_out/${TAG}_pmcnt_table.txt gpurun_out/${TAG}_pmcwg_table.txt | cut -c1-300 ;;
     pmc_lab)
       export TMPDIR=/tmp
       i=0
