@@ -9,6 +9,8 @@
 // Weight/bias gradients: each wave accumulates its rows' contribution for all
 // H columns in registers, writes one fp32 partial row, and a second kernel
 // sums the partials column-wise in a fixed order (deterministic, no atomics).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -94,15 +96,16 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x,
 // every global access of an iteration is unconditional and issued in the order
 // [x,dy(row + nwaves)] [dres(row)] [dx stores(row)], and w / dW live in LDS, so
 // phase 1 of a row never waits on the prefetch of the next one.
-template <typename T, int VPL>
+template <typename T, int VPL, bool R = false>
 struct RowRegs {
-  V16<T> x[VPL], g[VPL];
+  V16<T> x[VPL], g[VPL], r[R ? VPL : 1];
 };
 
-template <typename T, int VPL, bool FULL>
-__device__ __forceinline__ void load_row(RowRegs<T, VPL>& rr, const T* __restrict__ x,
+// R: the row's dres (residual-branch gradient) rides with x / dy, a row ahead
+template <typename T, int VPL, bool FULL, bool R = false>
+__device__ __forceinline__ void load_row(RowRegs<T, VPL, R>& rr, const T* __restrict__ x,
                                          const T* __restrict__ dy, int64_t row, int H, int lane,
-                                         int nvec) {
+                                         int nvec, const T* __restrict__ dres = nullptr) {
   constexpr int N = V16<T>::N;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
@@ -110,6 +113,7 @@ __device__ __forceinline__ void load_row(RowRegs<T, VPL>& rr, const T* __restric
     if (FULL || vi < nvec) {
       rr.x[i] = ld16(x + row * H + vi * N);
       rr.g[i] = ld16(dy + row * H + vi * N);
+      if constexpr (R) rr.r[i] = ld16(dres + row * H + vi * N);
     }
   }
 }
@@ -124,15 +128,18 @@ __device__ __forceinline__ lvec<T> lds_ld16(const T* p) {
   return *static_cast<const lvec<T>*>(__builtin_assume_aligned(p, 16));
 }
 
-template <typename T, int VPL, bool DW, bool FULL, bool DRES>
-__device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T, VPL>& nxt,
+// RA: dres prefetched a row ahead with x / dy (EMA_RMS_DRES_AHEAD=0: fetched
+// after the row's reduction, the round-4 form)
+template <typename T, int VPL, bool DW, bool FULL, bool DRES, bool RA>
+__device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL, RA>& rr, RowRegs<T, VPL, RA>& nxt,
                                             int64_t nrow, const T* __restrict__ x,
                                             const T* __restrict__ dy, float* __restrict__ acc,
                                             const T* __restrict__ w_lds, float r,
                                             const T* __restrict__ dres, T* __restrict__ dx,
                                             int64_t row, int H, int lane, int nvec) {
   constexpr int N = V16<T>::N;
-  load_row<T, VPL, FULL>(nxt, x, dy, nrow, H, lane, nvec);
+  static_assert(!RA || DRES, "dres ahead needs dres");
+  load_row<T, VPL, FULL, RA>(nxt, x, dy, nrow, H, lane, nvec, dres);
   float dot = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
@@ -160,8 +167,8 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
   // dres is fetched only now (its 32 VGPRs would otherwise overlap the phase-1
   // temporaries and spill); the wait for it also covers the prefetch, which
   // has had all of phase 1 to land.
-  V16<T> rv[DRES ? VPL : 1];
-  if (DRES) {
+  V16<T> rv[DRES && !RA ? VPL : 1];
+  if (DRES && !RA) {
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int vi = lane + i * 64;
@@ -180,7 +187,8 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
       for (int e = 0; e < N; ++e) {
         const float xh = to_f(rr.x[i].v[e]) * r;
         float v = r * (to_f(rr.g[i].v[e]) * to_f(wv[e]) - xh * dot);
-        if (DRES) v += to_f(rv[i].v[e]);
+        if constexpr (RA) v += to_f(rr.r[i].v[e]);
+        else if (DRES) v += to_f(rv[i].v[e]);
         o.v[e] = from_f<T>(v);
       }
       st16(dxr + vi * N, o);
@@ -195,7 +203,7 @@ __device__ __forceinline__ void rms_bwd_row(const RowRegs<T, VPL>& rr, RowRegs<T
 // consecutive 16-B slots (conflict-free; the natural [vi][q] order put lanes 32
 // bytes apart: 2-way conflicts, 4.3 conflict cycles per LDS instruction in
 // profiles/r1_llama7b_pmc_step.csv).
-template <typename T, int VPL, bool DW, bool FULL, bool DRES>
+template <typename T, int VPL, bool DW, bool FULL, bool DRES, bool RA = false>
 __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __restrict__ dy,
                                                         const T* __restrict__ x,
                                                         const T* __restrict__ w,
@@ -231,18 +239,18 @@ __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __re
     }
   }
   __syncthreads();
-  RowRegs<T, VPL> a, b;
+  RowRegs<T, VPL, RA> a, b;
   int64_t row = gw;
-  if (row < rows) load_row<T, VPL, FULL>(a, x, dy, row, H, lane, nvec);
+  if (row < rows) load_row<T, VPL, FULL, RA>(a, x, dy, row, H, lane, nvec, dres);
   // prefetches past the last row re-read row rows-1 (kept unconditional)
   while (row < rows) {
     int64_t nrow = row + nwaves;
-    rms_bwd_row<T, VPL, DW, FULL, DRES>(a, b, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
+    rms_bwd_row<T, VPL, DW, FULL, DRES, RA>(a, b, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
                                         rstd[row], dres, dx, row, H, lane, nvec);
     row = nrow;
     if (row >= rows) break;
     nrow = row + nwaves;
-    rms_bwd_row<T, VPL, DW, FULL, DRES>(b, a, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
+    rms_bwd_row<T, VPL, DW, FULL, DRES, RA>(b, a, nrow < rows ? nrow : rows - 1, x, dy, acc, w_lds,
                                         rstd[row], dres, dx, row, H, lane, nvec);
     row = nrow;
   }
@@ -570,7 +578,15 @@ void launch_rms_bwd(const void* dy, const void* x, const void* w, const float* r
                     const void* dres, void* dx, float* dw_part, int64_t rows, int H, int blocks,
                     hipStream_t s) {
   const size_t lds = (H * sizeof(T) + 15) / 16 * 16 + (DW ? kWaves * H * sizeof(float) : 0);
-  if (dres)
+  static const bool ahead = [] {
+    const char* e = getenv("EMA_RMS_DRES_AHEAD");
+    return !(e && e[0] == '0');
+  }();
+  if (dres && ahead)
+    hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, DW, FULL, true, true>), dim3(blocks), dim3(256), lds, s,
+                       (const T*)dy, (const T*)x, (const T*)w, rstd, (const T*)dres, (T*)dx,
+                       dw_part, rows, H);
+  else if (dres)
     hipLaunchKernelGGL((rmsnorm_bwd_k<T, V, DW, FULL, true>), dim3(blocks), dim3(256), lds, s,
                        (const T*)dy, (const T*)x, (const T*)w, rstd, (const T*)dres, (T*)dx,
                        dw_part, rows, H);

@@ -15,6 +15,7 @@
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
 #   profpx7    rocprofv3 kernel trace of the llama7b-tp8 proxy (profpx70: llama70b-tp8)
 #   ab         bench.py twice plain / twice with $AB_ENV, interleaved
+#   scriptab   python $SCRIPT plain / with $AB_ENV, interleaved twice
 #   ltre       scripts/lt_retune.py (torch.matmul's hipBLASLt pick vs the best solution)
 #   lab        scripts/gemm_lab.py (bench-only GEMM builds vs production vs hipBLASLt)
 #   gemm       scripts/gemm_nt_bench.py (in-model NT shapes vs hipBLASLt)
@@ -81,6 +82,12 @@ for step in "$@"; do
         echo "$f $(grep -o '"value": [0-9.]*' "$f")"
       done ;;
     ltre) run ltre 500 python -u scripts/lt_retune.py ;;
+    scriptab)  # $SCRIPT plain, then with $AB_ENV, interleaved twice
+      for i in 1 2; do
+        run "sab${i}a" 300 python -u $SCRIPT
+        run "sab${i}b" 300 env $AB_ENV python -u $SCRIPT
+      done
+      tail -n 5 gpurun_out/${TAG}_sab?[ab].log ;;
     lab) run lab 400 python -u scripts/gemm_lab.py $LAB_SHAPES ;;
     gemm) run gemm 400 python -u scripts/gemm_nt_bench.py --variants ${NT_VARIANTS:-5,6} ;;
     wgrad) run wgrad 400 python -u scripts/wgrad_ab.py ;;
