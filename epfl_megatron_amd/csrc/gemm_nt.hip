@@ -849,7 +849,7 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
   }
 }
 
-template <typename T, int EPI, int ACT>
+template <typename T, int EPI, int ACT, bool SPK = false>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   // (ablation builds of this structure: gemm_lab.hip, bench-only)
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
@@ -861,7 +861,8 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
   // split-K (EPI_STORE, few tiles): item = (split, tile), split-major; each
   // item runs nt = K / BK2 / ksplit K-steps from K-step ks * nt and stores
   // an fp32 partial tile, summed by gemm_nt_split_reduce_k
-  const int ksplit = EPI == EPI_STORE ? p.ksplit : 1;
+  static_assert(!SPK || EPI == EPI_STORE, "split-K: plain products only");
+  const int ksplit = SPK ? p.ksplit : 1;
   const int nitems = ntiles * ksplit;
   const int G = gridDim.x, bid = blockIdx.x;
   if (bid >= nitems) return;
@@ -1007,7 +1008,7 @@ __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
     int64_t m0, n0;
     int ks, lt;
     tile_org(i, m0, n0, ks, lt);
-    if (EPI == EPI_STORE && ksplit > 1) {
+    if constexpr (SPK) {
       // fp32 partial: the wave's 128 x 128 block of the dense 256 x 256 tile
       float* w = p.ws + ((int64_t)ks * ntiles + lt) * (TM * TN) + (128 * wm + (lane & 15)) * TN +
                  128 * wn + 4 * (lane >> 4);
@@ -1131,14 +1132,19 @@ void launch_one(const NtArgs& p, hipStream_t s) {
     const int64_t a_extent = p.am.rows == 0 ? (int64_t)p.M : (int64_t)TM;  // rows one descriptor spans
     if (g_var[EPI] == 6 && p.K % BK2 == 0 && p.K >= 2 * BK2 && maps_ok &&
         a_extent * p.lda * 2 < lim && brows * p.ldb * 2 < lim) {
-      const int items = p.ntm * p.ntn * (EPI == EPI_STORE && p.ws ? p.ksplit : 1);
-      const int g = std::min(items, num_cus());
+      if constexpr (EPI == EPI_STORE) {
+        if (p.ws && p.ksplit > 1) {  // few tiles: K split over fp32 partials
+          const int g = std::min(p.ntm * p.ntn * p.ksplit, num_cus());
+          hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT, true>), dim3(g), dim3(256), 0, s, p);
+          hipLaunchKernelGGL(gemm_nt_split_reduce_k<T>, dim3((unsigned)(p.ntm * p.ntn * 64)),
+                             dim3(256), 0, s, p);
+          return;
+        }
+      }
       NtArgs q = p;
-      if (!(EPI == EPI_STORE && p.ws)) q.ksplit = 1;
+      q.ksplit = 1;
+      const int g = std::min(p.ntm * p.ntn, num_cus());
       hipLaunchKernelGGL((gemm_nt6_k<T, EPI, ACT>), dim3(g), dim3(256), 0, s, q);
-      if (EPI == EPI_STORE && q.ksplit > 1)
-        hipLaunchKernelGGL(gemm_nt_split_reduce_k<T>, dim3((unsigned)(p.ntm * p.ntn * 64)), dim3(256),
-                           0, s, q);
       return;
     }
   }
