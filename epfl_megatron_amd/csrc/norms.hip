@@ -9,6 +9,7 @@
 // Weight/bias gradients: each wave accumulates its rows' contribution for all
 // H columns in registers, writes one fp32 partial row, and a second kernel
 // sums the partials column-wise in a fixed order (deterministic, no atomics).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -266,6 +267,100 @@ __global__ __launch_bounds__(256, DRES ? 1 : 2) void rmsnorm_bwd_k(const T* __re
         *reinterpret_cast<float4*>(part + vi * N + 4 * q) =
             *reinterpret_cast<const float4*>(acc + q * nvec * 4 + vi * 4);
   }
+}
+
+// One row per workgroup iteration (the row split over the 256 threads, EV
+// 16-B vectors each: H = 2048 EV for 16-bit types), rows strided by the grid,
+// the next row's x / dy / dres prefetched while the current one is reduced.
+// Registers stay ~100 per lane, so ~4 workgroups share a CU and keep 4x the
+// loads of the one-wave-per-row kernel (2 waves per SIMD at 256 VGPRs) in
+// flight.  The row's dot product crosses the 4 waves through a 2-slot LDS
+// pair (one barrier per row); the dW partial of the workgroup's rows stays in
+// registers (each thread owns the same columns on every row) and is written
+// once as a partial row for the ordered column sum.
+template <typename T, int EV, bool DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_wg_k(const T* __restrict__ dy,
+                                                        const T* __restrict__ x,
+                                                        const T* __restrict__ w,
+                                                        const float* __restrict__ rstd,
+                                                        const T* __restrict__ dres,
+                                                        T* __restrict__ dx,
+                                                        float* __restrict__ dw_part, int64_t rows,
+                                                        int H) {
+  constexpr int N = V16<T>::N;
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  struct Row {
+    V16<T> x[EV], g[EV], r[DRES ? EV : 1];
+  };
+  auto load = [&](Row& rr, int64_t row) {
+#pragma unroll
+    for (int e = 0; e < EV; ++e) {
+      const int64_t o = row * H + (int64_t)(tid + 256 * e) * N;
+      rr.x[e] = ld16(x + o);
+      rr.g[e] = ld16(dy + o);
+      if constexpr (DRES) rr.r[e] = ld16(dres + o);
+    }
+  };
+  V16<T> wr[EV];
+#pragma unroll
+  for (int e = 0; e < EV; ++e) wr[e] = ld16(w + (tid + 256 * e) * N);
+  float acc[EV][N];
+#pragma unroll
+  for (int e = 0; e < EV; ++e)
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[e][k] = 0.f;
+  const int64_t G = gridDim.x;
+  int par = 0;
+  auto step = [&](const Row& cur, Row& nxt, int64_t row) {
+    const int64_t nrow = row + G;
+    if (nrow < rows) load(nxt, nrow);
+    const float r = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int e = 0; e < EV; ++e)
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const float xh = to_f(cur.x[e].v[k]) * r;
+        const float g = to_f(cur.g[e].v[k]);
+        dot += g * to_f(wr[e].v[k]) * xh;
+        acc[e][k] += g * to_f(from_f<T>(xh));
+      }
+    dot = wave_sum(dot);
+    if (lane == 0) red[par][wv] = dot;
+    __syncthreads();
+    dot = (red[par][0] + red[par][1] + red[par][2] + red[par][3]) / (float)H;
+    par ^= 1;
+#pragma unroll
+    for (int e = 0; e < EV; ++e) {
+      V16<T> o;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const float xh = to_f(cur.x[e].v[k]) * r;
+        float v = r * (to_f(cur.g[e].v[k]) * to_f(wr[e].v[k]) - xh * dot);
+        if constexpr (DRES) v += to_f(cur.r[e].v[k]);
+        o.v[k] = from_f<T>(v);
+      }
+      st16(dx + row * H + (int64_t)(tid + 256 * e) * N, o);
+    }
+  };
+  Row a, b;
+  int64_t row = blockIdx.x;
+  if (row < rows) load(a, row);
+  while (row < rows) {
+    step(a, b, row);
+    row += G;
+    if (row >= rows) break;
+    step(b, a, row);
+    row += G;
+  }
+  float* part = dw_part + (int64_t)blockIdx.x * H;
+#pragma unroll
+  for (int e = 0; e < EV; ++e)
+#pragma unroll
+    for (int k = 0; k < N; k += 4)
+      *reinterpret_cast<float4*>(part + (tid + 256 * e) * N + k) =
+          make_float4(acc[e][k], acc[e][k + 1], acc[e][k + 2], acc[e][k + 3]);
 }
 
 template <typename T, int VPL>
@@ -596,11 +691,49 @@ void launch_rms_bwd(const void* dy, const void* x, const void* w, const float* r
                        dw_part, rows, H);
 }
 
+// EMA_RMS_BWD_WG=0: the one-wave-per-row backward everywhere (A/B)
+bool rms_bwd_wg_on() {
+  static const bool on = [] {
+    const char* e = getenv("EMA_RMS_BWD_WG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
                  const void* dres, void* dx, float* dw_part, void* dw, float* dw_acc,
                  int accumulate, int64_t rows, int H, int dt, hipStream_t s) {
   const int P = norm_bwd_partials(rows);
   const int blocks = P / kWaves;
+  // workgroup-per-row form: 16-bit types, H = 2048 EV (EV 1, 2, 4), enough
+  // rows to fill the grid; its partial rows (one per workgroup, <= P) go to
+  // the same column sum
+  const int ev = H % 2048 == 0 ? H / 2048 : 0;
+  if (rms_bwd_wg_on() && dt != DT_F32 && (ev == 1 || ev == 2 || ev == 4) && rows >= 4 * 256) {
+    // one resident wave of workgroups (registers allow ~5 / 3 / 1 per CU at
+    // EV = 1 / 2 / 4): every partial row written once, no second round
+    const int per_cu = ev == 1 ? 5 : ev == 2 ? 3 : 1;
+    const int G = (int)std::min<int64_t>(std::min<int64_t>(P, 256 * per_cu), rows / 4);
+#define EMA_RMS_WG(T_, EV_)                                                                        \
+    {                                                                                             \
+      if (dres)                                                                                   \
+        hipLaunchKernelGGL((rmsnorm_bwd_wg_k<T_, EV_, true>), dim3(G), dim3(256), 0, s,           \
+                           (const T_*)dy, (const T_*)x, (const T_*)w, rstd, (const T_*)dres,      \
+                           (T_*)dx, dw_part, rows, H);                                            \
+      else                                                                                        \
+        hipLaunchKernelGGL((rmsnorm_bwd_wg_k<T_, EV_, false>), dim3(G), dim3(256), 0, s,          \
+                           (const T_*)dy, (const T_*)x, (const T_*)w, rstd, (const T_*)dres,      \
+                           (T_*)dx, dw_part, rows, H);                                            \
+      colsum<T_>(dw_part, (T_*)dw, dw_acc, accumulate, G, H, s);                                  \
+    }
+    if (dt == DT_BF16) {
+      if (ev == 1) EMA_RMS_WG(bf16, 1) else if (ev == 2) EMA_RMS_WG(bf16, 2) else EMA_RMS_WG(bf16, 4)
+    } else {
+      if (ev == 1) EMA_RMS_WG(fp16, 1) else if (ev == 2) EMA_RMS_WG(fp16, 2) else EMA_RMS_WG(fp16, 4)
+    }
+#undef EMA_RMS_WG
+    return;
+  }
   EMA_DISPATCH_FLOAT(dt, T, {
     const int vpl = pick_vpl<T>(H);
     const bool full = H == vpl * 64 * (16 / (int)sizeof(T));

@@ -52,6 +52,27 @@ def test_rmsnorm(dtype, H):
     _close(w.grad, wr.grad, 0.5 if dtype != torch.float32 else 1e-3, 2e-2, "rmsnorm dw")
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("rows,H", [(1100, 2048), (2501, 4096), (1500, 8192)])
+def test_rmsnorm_many_rows(dtype, rows, H):
+    """Training-size row counts: the workgroup-per-row backward (EV = 1 / 2 / 4
+    vectors per thread, odd trip counts of its two-row loop, dW partials of
+    one resident wave of workgroups) against the fp32 reference."""
+    from epfl_megatron_amd.ops.norms import rms_norm, rms_norm_ref
+    torch.manual_seed(rows)
+    x = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(dtype).requires_grad_()
+    y = rms_norm(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = rms_norm_ref(xr, wr, 1e-5)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    _close(x.grad, xr.grad, 5e-2, 2e-2, "rmsnorm dx")
+    _close(w.grad, wr.grad, 0.02 * rows ** 0.5, 2e-2, "rmsnorm dw")
+
+
 @pytest.mark.parametrize("is_rms", [True, False])
 @pytest.mark.parametrize("with_res", [True, False])
 @pytest.mark.parametrize("rows,H", [(37, 4096), (5003, 4096), (129, 12288)])
