@@ -616,6 +616,17 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
             mfma_vgpr<T>(dpacc, va, df[kk]);
           }
         }
+        // K^T fragments of this 32-key sub-block (asm transposed reads), issued
+        // before the softmax VALU so their latency hides under it (retired by
+        // one lds_wait before the dS K MFMAs, as the dK/dV kernel does)
+        typename MT<T>::x4 kt[2][DT][2];
+        static_for<2>([&](auto sc) {
+          static_for<DT>([&](auto dc) {
+            constexpr int o = sub * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
+            kt[sc][dc][0] = tr_read_imm<o, T>(trv0);
+            kt[sc][dc][1] = tr_read_imm<o, T>(trv1);
+          });
+        });
         mfma_drain();
         const bool need_mask = (kb + 32 > p.sk) || (q0w + 32 > p.sq) ||
                                (CAUSAL && (kb + 31 > q0w + off || kb < ds_wmax));
@@ -653,14 +664,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
           sacc[i] = d[0];
           sacc[i + 1] = d[1];
         }
+        lds_wait();  // the K^T reads above
         static_for<2>([&](auto sc) {
           const x8 sf = acc_frag<T>(sacc, decltype(sc)::value);
           static_for<DT>([&](auto dc) {
-            constexpr int o = sub * 4 * RG + decltype(sc)::value * 2 * RG + 512 * decltype(dc)::value;
-            const typename MT<T>::x4 k0 = tr_read_imm<o, T>(trv0);
-            const typename MT<T>::x4 k1 = tr_read_imm<o, T>(trv1);
-            lds_wait();
-            mfma_vgpr<T, 1>(dq[dc], join<T>(k0, k1), sf);
+            mfma_vgpr<T, 1>(dq[dc], join<T>(kt[sc][dc][0], kt[sc][dc][1]), sf);
           });
         });
       });
