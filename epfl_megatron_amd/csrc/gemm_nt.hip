@@ -1067,13 +1067,21 @@ int nt_ksplit(int tiles, int64_t K) {
   return best;
 }
 
+// Tile grouping of the persistent kernel's tile order (tile_of): groups of 4
+// m-tiles x all n-tiles.  Measured against the round-4 rule (8 m-tiles, or 8
+// n-tiles when M has more tiles) on the 7B shapes, one box
+// (profiles/r6t_gemm_group_sweep.txt): fc1 + GLU +3.8 %, fc2 dgrad + dGLU
+// +2.7 %, plain products +0.5 %.  EMA_GEMM_GM=<g> overrides (> 0: groups of g
+// m-tiles, < 0: groups of -g n-tiles); EMA_GEMM_GM=old restores the old rule.
 int group_m(int ntm, int ntn) {
   static const int env = [] {
     const char* e = getenv("EMA_GEMM_GM");
+    if (e && e[0] == 'o') return 1 << 20;
     return e ? atoi(e) : 0;
   }();
+  if (env == 1 << 20) return ntm <= ntn ? 8 : -8;
   if (env != 0) return env;
-  return ntm <= ntn ? 8 : -8;
+  return 4;
 }
 
 #define EMA_GLU_KIND2(kind, ...)                              \
