@@ -140,6 +140,38 @@ def build_sanitized(kind, out_dir):
     return exe
 
 
+def build_lab(force=False):
+    """Bench-only GEMM lab (``scripts/lab``): ``scripts/lab/_gemm_lab.so``.
+    Not part of ``build_all``: nothing in the framework loads it."""
+    lab = os.path.join(os.path.dirname(PKG), "scripts", "lab")
+    out = os.path.join(lab, "_gemm_lab.so")
+    srcs = [os.path.join(lab, "gemm_lab.hip"), os.path.join(lab, "lab_bindings.cpp")]
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    if not (force or _newer(out, srcs + headers)):
+        return out
+    inc, lib, abi = _torch_paths()
+    objs = []
+    for src in srcs:
+        obj = os.path.join(BUILD, "lab_" + os.path.basename(src) + ".o")
+        cmd = [HIPCC, "-c", src, "-o", obj, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+               "-I", CSRC, "-Wno-unused-result"]
+        if src.endswith(".cpp"):
+            cmd += [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_gemm_lab",
+                    "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                    "-I", sysconfig.get_paths()["include"], "-Wno-deprecated-declarations"]
+            for i in inc:
+                cmd += ["-I", i]
+        else:
+            cmd += ["-mcode-object-version=5"]
+        os.makedirs(BUILD, exist_ok=True)
+        _run(cmd)
+        objs.append(obj)
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs +
+         ["-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+          "-ltorch_python", f"-Wl,-rpath,{lib}"])
+    return out
+
+
 def build_all(force=False, jobs=None):
     build_dedup(force)
     h = build_data_helpers(force)
@@ -152,7 +184,10 @@ def main():
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--only", choices=["kernels", "data"], default=None)
+    ap.add_argument("--lab", action="store_true", help="also build the bench-only GEMM lab")
     a = ap.parse_args()
+    if a.lab:
+        print(build_lab(a.force))
     if a.only == "data":
         print(build_data_helpers(a.force))
     elif a.only == "kernels":

@@ -234,6 +234,8 @@ def wait_for_async_save():
 
 def save_checkpoint(iteration, model, optimizer, opt_param_scheduler):
     args = global_vars.get_args()
+    from .parallel import comm  # noqa: PLC0415
+    comm.check_xgmi()  # never write weights computed after a timed-out xGMI wait
     if optimizer is not None:
         optimizer.resolve_pending()   # settle a lazily-checked skipped step
         optimizer.wait_param_sync()   # dist-opt parameter all-gather in flight

@@ -234,8 +234,9 @@ FLAG_TABLE = {
               help="MI355X per-rank proxy: build and run ONE tensor-parallel rank of a "
                    "TP=N model in this process (sharded weights, heads, vocab and, with "
                    "--sequence_parallel, s/N-row norms / residuals / dropout). TP "
-                   "collectives become local loopbacks (all-gather replicates the shard, "
-                   "reduce-scatter takes the mean of the N chunks) that are accounted in "
+                   "collectives become local loopbacks (all-gather writes the shard into "
+                   "every rank's slot, reduce-scatter keeps this rank's own chunk without "
+                   "reducing, all-reduce / broadcast are identities) that are accounted in "
                    "the comm table with the bytes a real rank would send"),
         _flag("--ddp_comm_groups", type=int, default=1,
               help="communicators over the DP ranks; DDP buckets are issued round-robin "
@@ -250,6 +251,17 @@ FLAG_TABLE = {
                    "one-shot xGMI kernel (default: --tp_xgmi_allreduce_kb).  Sized for the "
                    "sequence-parallel [s/tp, b, h] pieces (multi-MiB) it lets the all-gather "
                    "take the W-1 links at once instead of an RCCL ring"),
+        _flag("--tp_xgmi_timeout_ms", type=int, default=None,
+              help="wall-clock bound (ms) of a one-shot xGMI collective's wait on a peer "
+                   "(default 60000, or EMA_XGMI_TIMEOUT_MS): long, so a late but healthy "
+                   "rank never trips it; a timed-out wait NaN-fills the output, skips the "
+                   "optimizer step on every rank and raises at the next log / checkpoint"),
+        _flag("--sp_regather_inputs", action="store_true",
+              help="sequence parallel: all-gather the inputs of the column-parallel products "
+                   "(QKV, fc1, LM head) again in the backward for their weight gradients, as "
+                   "the reference does, instead of keeping the forward's gathered copies "
+                   "(default: kept; 2 fewer full-size TP collectives per layer and "
+                   "micro-batch for [s, b, h] of HBM per product)"),
         _flag("--no_overlap_grad_reduce", action="store_false", dest="overlap_grad_reduce"),
         _flag("--no_overlap_param_gather", action="store_false", dest="overlap_param_gather",
               help="dist-opt: all-gather parameters synchronously at step end instead of "

@@ -47,8 +47,10 @@ __global__ __launch_bounds__(256) void glu_bwd_k(const T* __restrict__ dy, const
 #pragma unroll
   for (int e = 0; e < N; ++e) {
     const float gv = to_f(g.v[e]), dv = to_f(d.v[e]);
-    da.v[e] = from_f<T>(dv * act<KIND>(gv));
-    dg.v[e] = from_f<T>(dv * to_f(a.v[e]) * dact<KIND>(gv));
+    float av, dd;
+    act_dact<KIND>(gv, av, dd);
+    da.v[e] = from_f<T>(dv * av);
+    dg.v[e] = from_f<T>(dv * to_f(a.v[e]) * dd);
   }
   T* dr = dx + r * (2 * (int64_t)F);
   st16(dr + c, da);

@@ -345,17 +345,22 @@ at::Tensor softmax_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& mas
   if (mode == 1) TORCH_CHECK(SQ == SK, "causal softmax expects square scores");
   const uint8_t* mp = nullptr;
   at::Tensor m;
+  int64_t mask_bs = 0;
   if (mode == 2) {
     TORCH_CHECK(mask.has_value() && mask->defined(), "mask required for mode 2");
-    m = mask->to(at::kByte).contiguous();
-    TORCH_CHECK(m.dim() == 4 && m.size(0) == B && m.size(1) == 1 && m.size(2) == SQ && m.size(3) == SK,
-                "mask must be [b, 1, sq, sk]");
+    // bool -> uint8 is a reinterpretation (same bytes), no copy
+    m = mask->scalar_type() == at::kBool ? mask->view(at::kByte) : mask->to(at::kByte);
+    m = m.contiguous();
+    TORCH_CHECK(m.dim() == 4 && (m.size(0) == B || m.size(0) == 1) && m.size(1) == 1 &&
+                    m.size(2) == SQ && m.size(3) == SK,
+                "mask must be [b or 1, 1, sq, sk]");
+    mask_bs = m.size(0) == 1 ? 0 : (int64_t)SQ * SK;  // a batch-broadcast mask is never expanded
     mp = m.data_ptr<uint8_t>();
   }
   auto y = at::empty_like(x);
   if (x.numel() > 0)
-    ema::softmax_fwd(x.data_ptr(), mp, y.data_ptr(), B, NP, SQ, SK, (float)scale, (int)mode,
-                     dtype_code(x), cur_stream());
+    ema::softmax_fwd(x.data_ptr(), mp, mask_bs, y.data_ptr(), B, NP, SQ, SK, (float)scale,
+                     (int)mode, dtype_code(x), cur_stream());
   return y;
 }
 
@@ -955,8 +960,10 @@ at::Tensor bias_dropout_add_bwd(const at::Tensor& dout, double p, int64_t seed, 
 // ---------------------------------------------------------------- wgrad GEMM
 bool wgrad_supported(int64_t M, int64_t N, int64_t K) { return ema::wgrad_supported(M, N, K); }
 
-// main_grad[N,K] (+)= dy[M,N]^T x[M,K]
-void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool accumulate) {
+// main_grad[N,K] (+)= dy[M,N]^T x[M,K]; x_map = [rows, n1, s1, s2]: dY's token
+// q pairs with X row ((q / rows) % n1) * s1 + ((q / rows) / n1) * s2 + q % rows
+void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool accumulate,
+                std::vector<int64_t> x_map) {
   check_gpu(dy, "dy");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && g.dim() == 2, "wgrad_gemm: 2-D operands");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && g.is_contiguous(),
@@ -964,7 +971,23 @@ void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool ac
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && g.scalar_type() == at::kFloat,
               "wgrad_gemm: dy/x same 16-bit dtype, g fp32");
   const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
-  TORCH_CHECK(x.size(0) == M && g.size(0) == N && g.size(1) == K, "wgrad_gemm: shape mismatch");
+  TORCH_CHECK(g.size(0) == N && g.size(1) == K, "wgrad_gemm: shape mismatch");
+  ema::TokMap xm;
+  if (x_map.empty()) {
+    TORCH_CHECK(x.size(0) == M, "wgrad_gemm: shape mismatch");
+  } else {
+    TORCH_CHECK(x_map.size() == 4, "wgrad_gemm: x_map = [rows, n1, s1, s2]");
+    const int64_t R = x_map[0], n1 = x_map[1], s1 = x_map[2], s2 = x_map[3];
+    TORCH_CHECK(R > 0 && R % 32 == 0 && n1 > 0 && s1 >= 0 && s2 >= 0 && M % (R * n1) == 0,
+                "wgrad_gemm: x_map rows must be a positive multiple of 32 dividing M / n1");
+    const int64_t n2 = M / (R * n1);
+    TORCH_CHECK((n1 - 1) * s1 + (n2 - 1) * s2 + R <= x.size(0),
+                "wgrad_gemm: x_map reaches past the rows of x");
+    xm.rows = (int)R;
+    xm.n1 = (int)n1;
+    xm.s1 = s1;
+    xm.s2 = s2;
+  }
   TORCH_CHECK(ema::wgrad_supported(M, N, K), "wgrad_gemm: unsupported shape");
   const int dt = dtype_code(dy);
   TORCH_CHECK(dt == ema::DT_BF16 || dt == ema::DT_F16, "wgrad_gemm: bf16/fp16 only");
@@ -974,7 +997,7 @@ void wgrad_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor g, bool ac
   at::Tensor ws;
   if (wsf > 0) ws = at::empty({wsf}, g.options());
   ema::wgrad_gemm(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), M, N, K, accumulate, dt,
-                  cur_stream(), wsf > 0 ? ws.data_ptr<float>() : nullptr);
+                  cur_stream(), wsf > 0 ? ws.data_ptr<float>() : nullptr, xm);
 }
 
 // (main_tiles, tail_lin0, tail_tiles, nsplit) of a wgrad shape
@@ -1194,26 +1217,16 @@ void register_gemm_lt(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
-  m.def("wgrad_gemm", &wgrad_gemm);
+  m.def("wgrad_gemm", &wgrad_gemm, py::arg("dy"), py::arg("x"), py::arg("g"),
+        py::arg("accumulate"), py::arg("x_map") = std::vector<int64_t>{});
   m.def("wgrad_supported", &wgrad_supported);
   m.def("wgrad_set_variant", &ema::wgrad_set_variant);
-  m.def("gemm_lab", [](const at::Tensor& a, const at::Tensor& b, at::Tensor c, int64_t variant) {
-    TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
-                    c.scalar_type() == at::kBFloat16 && a.is_contiguous() && b.is_contiguous() &&
-                    c.is_contiguous() && a.size(1) == b.size(1) && c.size(0) == a.size(0) &&
-                    c.size(1) == b.size(0) && a.size(1) % 64 == 0 && a.size(1) >= 128 &&
-                    b.size(0) % 8 == 0,
-                "gemm_lab: contiguous bf16 [M,K] x [N,K] -> [M,N], K % 64 == 0, K >= 128");
-    TORCH_CHECK(a.size(0) * a.size(1) * 2 < (int64_t(1) << 31) && b.size(0) * b.size(1) * 2 < (int64_t(1) << 31),
-                "gemm_lab: operands must be < 2 GiB (32-bit buffer offsets)");
-    ema::gemm_lab(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.size(0), b.size(0), a.size(1),
-                  (int)variant, cur_stream());
-  });
   m.def("wgrad_plan", &wgrad_plan);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out") = py::none(),
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},
         py::arg("m") = 0);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_ksplit", [](int64_t M, int64_t N, int64_t K) { return ema::gemm_nt_ksplit(M, N, K); });
   m.def("gemm_nt_set_variant", &ema::gemm_nt_set_variant);
   m.def("gemm_nt_glu", &gemm_nt_glu, py::arg("a"), py::arg("w1"), py::arg("kind"),
         py::arg("pre") = py::none(), py::arg("y") = py::none(),
@@ -1267,6 +1280,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_all_reduce", &xgmi_all_reduce);
   m.def("xgmi_all_gather", &xgmi_all_gather);
   m.def("xgmi_error", [](int64_t id) { return ema::xgmi_error(id); });
+  m.def("xgmi_set_timeout", [](int64_t id, int64_t ms) { ema::xgmi_set_timeout(id, ms); });
+  m.def("xgmi_get_timeout", [](int64_t id) { return ema::xgmi_get_timeout(id); });
+  m.def("xgmi_error_tensor", [](int64_t id) {
+    // a view of the communicator's device error word (no ownership: the
+    // Python communicator keeps it alive while it holds the view)
+    int dev = 0;
+    TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+    return at::from_blob(ema::xgmi_error_word(id), {1},
+                         at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
+  });
   m.def("xgmi_destroy", [](int64_t id) { ema::xgmi_destroy(id); });
   m.def("flash_decode", &flash_decode, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"),
         py::arg("b"), py::arg("sk"), py::arg("nq"), py::arg("nkv"), py::arg("hd"), py::arg("qs"),

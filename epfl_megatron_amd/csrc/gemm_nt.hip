@@ -227,9 +227,11 @@ __device__ __forceinline__ void epilogue_rows(const NtArgs& p, const char* reg, 
           V da, dg;
 #pragma unroll
           for (int e = 0; e < V::N; ++e) {
-            const float gv = to_f(g.v[e]), xg = to_f(x2[k].v[e]);
-            da.v[e] = from_f<T>(gv * act<ACT>(xg));
-            dg.v[e] = from_f<T>(gv * to_f(x1[k].v[e]) * dact<ACT>(xg));
+            const float gv = to_f(g.v[e]);
+            float av, dv;
+            act_dact<ACT>(to_f(x2[k].v[e]), av, dv);
+            da.v[e] = from_f<T>(gv * av);
+            dg.v[e] = from_f<T>(gv * to_f(x1[k].v[e]) * dv);
           }
           if (nok && gm < M) {
             st16(d + gm * p.ldc + gn, da);
@@ -834,9 +836,11 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
         V da, dg;
 #pragma unroll
         for (int e = 0; e < V::N; ++e) {
-          const float gf = to_f(g.v[e]), xg = to_f(x2[sl][jp].v[e]);
-          da.v[e] = from_f<T>(gf * act<ACT>(xg));
-          dg.v[e] = from_f<T>(gf * to_f(x1[sl][jp].v[e]) * dact<ACT>(xg));
+          const float gf = to_f(g.v[e]);
+          float av, dv;
+          act_dact<ACT>(to_f(x2[sl][jp].v[e]), av, dv);
+          da.v[e] = from_f<T>(gf * av);
+          dg.v[e] = from_f<T>(gf * to_f(x1[sl][jp].v[e]) * dv);
         }
         const int64_t f = gn0 + 32 * jp + 8 * q;
         if (rok && f < N) {
@@ -851,7 +855,7 @@ __device__ __forceinline__ void epilogue_regs(const NtArgs& p, const f32x4 (&acc
 
 template <typename T, int EPI, int ACT, bool SPK = false>
 __global__ void __launch_bounds__(256, 1) gemm_nt6_k(NtArgs p) {
-  // (ablation builds of this structure: gemm_lab.hip, bench-only)
+  // (ablation builds of this structure: scripts/lab/gemm_lab.hip, bench-only)
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   const int lane = threadIdx.x & 63;
@@ -1198,6 +1202,11 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
   return M > 0 && N > 0 && K > 0 && K % BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % 8 == 0 && M < ((int64_t)1 << 31) && N < ((int64_t)1 << 30) &&
          ((M + TM - 1) / TM) * ((N + TN / 2 - 1) / (TN / 2)) < ((int64_t)1 << 31);
+}
+
+int gemm_nt_ksplit(int64_t M, int64_t N, int64_t K) {
+  if (g_var[EPI_STORE] != 6) return 1;
+  return nt_ksplit((int)(((M + TM - 1) / TM) * ((N + TN - 1) / TN)), K);
 }
 
 int64_t gemm_nt_workspace_floats(int64_t M, int64_t N, int64_t K) {

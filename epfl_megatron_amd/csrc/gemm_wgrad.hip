@@ -51,6 +51,7 @@
 // ragged last tile row / column (e.g. the TP=8 shards of Llama-2-7B's FFN,
 // 2752 and 1376) clamps its loads and masks its stores.
 #include <cstdlib>
+#include <stdexcept>
 
 #include "fa_common.h"
 #include "gemm_plan.h"
@@ -142,10 +143,17 @@ __device__ __forceinline__ f32x4 mfma16(typename fa::MT<T>::x8 a, typename fa::M
   else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// physical X row of logical token q (TokMap in kernels.h)
+__device__ __forceinline__ int64_t tok_row(int64_t q, const TokMap& m) {
+  if (m.rows == 0) return q;
+  const int64_t grp = q / m.rows;
+  return (grp % m.n1) * m.s1 + (grp / m.n1) * m.s2 + (q - grp * m.rows);
+}
+
 template <typename T, bool ACCUM>
 __global__ void __launch_bounds__(512, 1)
 wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
-        int K, int gn, int msplit, float* __restrict__ ws, int lin0, int nlin) {
+        int K, int gn, int msplit, float* __restrict__ ws, int lin0, int nlin, TokMap xm) {
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -165,11 +173,12 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
   const int tn = tt.x, tk = tt.y;
   int64_t n0 = (int64_t)tn * TN, k0 = (int64_t)tk * TK;
   int ldg = K;  // row stride of the output
+  int64_t xq0 = 0;  // logical token of this workgroup's first X row (split-K offset)
   if (ws) {
     const int m0s = split * msplit;
     M = min(msplit, M - m0s);
     dy += (int64_t)m0s * N;
-    x += (int64_t)m0s * K;
+    xq0 = m0s;
     g = ws + ((int64_t)split * nlin + (lin - lin0)) * (TN * TK);
     ldg = TK;
   }
@@ -193,10 +202,12 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     }
   const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
 
+  // X rows of subtile t: 32 consecutive physical rows from tok_row(first)
+  auto xrow = [&](int t) { return tok_row(xq0 + (int64_t)t * BM, xm); };
   auto stage = [&](int t) {  // slot t % NSLOT <- tokens [t*BM, t*BM + BM)
     const int dst = (t % NSLOT) * SLOTB;
     stage_op<T>(dy, N, (int64_t)t * BM, n0, lds, dst, wave, lane);
-    stage_op<T>(x, K, (int64_t)t * BM, k0, lds, dst + OPB, wave, lane);
+    stage_op<T>(x, K, xrow(t), k0, lds, dst + OPB, wave, lane);
   };
 
   const int nt = M / BM;
@@ -210,8 +221,8 @@ wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g
     const int dst = (ts % NSLOT) * SLOTB;
     if (q == 0) stage_op<T, 0, 1>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
     else if (q == 1) stage_op<T, 1, 2>(dy, N, (int64_t)ts * BM, n0, lds, dst, wave, lane);
-    else if (q == 2) stage_op<T, 0, 1>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
-    else stage_op<T, 1, 2>(x, K, (int64_t)ts * BM, k0, lds, dst + OPB, wave, lane);
+    else if (q == 2) stage_op<T, 0, 1>(x, K, xrow(ts), k0, lds, dst + OPB, wave, lane);
+    else stage_op<T, 1, 2>(x, K, xrow(ts), k0, lds, dst + OPB, wave, lane);
   };
   typename fa::MT<T>::x4 fa_[FA_][2], fb_[FB_][2];
   auto reads = [&](int t) {  // all fragments of subtile t (24 transposed reads)
@@ -574,14 +585,14 @@ int tile_group(int ntn, int ntk) {
 
 template <typename T, bool ACCUM>
 void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
-            int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1) {
+            int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1, TokMap xm = {}) {
   const int ntiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
   if (nlin < 0) nlin = ntiles;
   const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
   hipLaunchKernelGGL((wgrad_k<T, ACCUM>), dim3(nlin * nsplit), dim3(512), 0, s,
                      (const T*)dy, (const T*)x, g, M, N, K,
                      tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), msplit,
-                     nsplit > 1 ? ws : nullptr, lin0, nlin);
+                     nsplit > 1 ? ws : nullptr, lin0, nlin, xm);
 }
 
 // G[tile] (+)= sum over the token splits of ws[split][tile] (fixed order) for
@@ -698,12 +709,13 @@ void launch4(const void* dy, const void* x, float* g, int M, int N, int K, int t
 }
 
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
-                bool accumulate, int dt, hipStream_t s, float* ws) {
+                bool accumulate, int dt, hipStream_t s, float* ws, TokMap xm) {
   const int iM = (int)M, iN = (int)N, iK = (int)K;
   const WgradPlan pl = wgrad_plan(M, N, K);
   const bool split = pl.nsplit > 1 && ws != nullptr;
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
-  if (main_tiles > 0 && wgrad4_ok(M, N, K)) {
+  if (xm.rows != 0 && xm.rows % BM != 0) throw std::runtime_error("wgrad: token map groups must be 32-row multiples");
+  if (main_tiles > 0 && xm.rows == 0 && wgrad4_ok(M, N, K)) {
     if (dt == DT_BF16) {
       if (accumulate) launch4<bf16, true>(dy, x, g, iM, iN, iK, main_tiles, s);
       else launch4<bf16, false>(dy, x, g, iM, iN, iK, main_tiles, s);
@@ -714,18 +726,18 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   } else
   if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<bf16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
+      else launch<bf16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
     } else if (dt == DT_F16) {
-      if (accumulate) launch<fp16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
-      else launch<fp16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles);
+      if (accumulate) launch<fp16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
+      else launch<fp16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
     }
   }
   if (split) {
     if (dt == DT_BF16)
-      launch<bf16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<bf16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
     else if (dt == DT_F16)
-      launch<fp16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles);
+      launch<fp16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
                        ws, g, iN, iK, tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK),
                        pl.tail_lin0, pl.tail_tiles,

@@ -60,8 +60,8 @@ void ce_bwd(const void* logits, const int64_t* target, const float* lse, const f
 
 // ---- softmax.hip -------------------------------------------------------------------
 // x [B, NP, SQ, SK]; mask (mode 2) uint8/bool [B, 1, SQ, SK]; mode 0 none, 1 causal.
-void softmax_fwd(const void* x, const uint8_t* mask, void* y, int64_t B, int64_t NP, int SQ,
-                 int SK, float scale, int mode, int dt, hipStream_t s);
+void softmax_fwd(const void* x, const uint8_t* mask, int64_t mask_bs, void* y, int64_t B,
+                 int64_t NP, int SQ, int SK, float scale, int mode, int dt, hipStream_t s);
 void softmax_bwd(const void* dy, const void* y, void* dx, int64_t rows, int SK, float scale,
                  int dt, hipStream_t s);
 
@@ -225,6 +225,9 @@ void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int 
 // out [world * nbytes] = every rank's in [nbytes], rank-major (in: disjoint or one chunk of out)
 void xgmi_all_gather(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s);
 int xgmi_error(int64_t id);
+void xgmi_set_timeout(int64_t id, int64_t ms);
+int64_t xgmi_get_timeout(int64_t id);
+void* xgmi_error_word(int64_t id);  // device int32, nonzero after a timed-out wait
 void xgmi_destroy(int64_t id);
 
 // ---- gemm_wgrad.hip ------------------------------------------------------------------------------
@@ -239,13 +242,20 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K);
 void wgrad_set_variant(int v);  // 8: 8-wave ping-pong (default), 4: persistent 4-wave kernel
 WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K);
 int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
+// Token (row) order of X relative to dY in a wgrad: logical token q of dY is
+// X's physical row
+//   ((q / rows) % n1) * s1 + ((q / rows) / n1) * s2 + q % rows   (rows == 0: q)
+// i.e. a two-level permutation of rows-sized groups.  It pairs the SP
+// pipeline's piece-major gathers ([piece][rank][R] rows) with natural-order
+// ([rank][piece][R]) rows without a permutation copy (parallel/tensor/
+// layers.py).  rows % 32 == 0 (a 32-token subtile never crosses a group).
+struct TokMap {
+  int rows = 0, n1 = 1;
+  int64_t s1 = 0, s2 = 0;
+};
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
-                bool accumulate, int dt, hipStream_t s, float* ws = nullptr);
+                bool accumulate, int dt, hipStream_t s, float* ws = nullptr, TokMap xmap = {});
 // ---- gemm_nt.hip: C[M,N] = A[M,K] B[N,K]^T (forward / dgrad), GLU epilogues --
-// Bench-only GEMM experiments (gemm_lab.hip): C = A B^T bf16, variant 0 =
-// production LDS layout, 1 = linear-source padded layout.
-void gemm_lab(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int variant,
-              hipStream_t s);
 void gemm_nt_set_variant(int v);  // 4 or 8 waves per workgroup
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 // Row-group remap of an operand's rows (the chunked TP all-gather / reduce-
@@ -260,6 +270,7 @@ void gemm_nt(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_
              float* ws = nullptr);
 // fp32 workspace (floats) gemm_nt splits K into for few-tile products (0: none)
 int64_t gemm_nt_workspace_floats(int64_t M, int64_t N, int64_t K);
+int gemm_nt_ksplit(int64_t M, int64_t N, int64_t K);  // K split the plain product runs with
 // fc1 forward: b = W1 [2F, K]; writes pre [M, 2F] and y = x1 * act(x2) [M, F]
 // (rows of both outputs through cmap)
 void gemm_nt_glu(const void* a, const void* b, void* pre, void* y, int64_t M, int64_t F,

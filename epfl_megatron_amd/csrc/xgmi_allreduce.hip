@@ -142,9 +142,24 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_oneshot_k(const XgArgs a) {
   if (t == 0) a.epoch[b] = e;
 }
 
+// Wall-clock bound of a peer wait (ms).  Long by default: TP ranks drift apart
+// through host work (a checkpoint write, first-iteration setup, a GC pause),
+// and a healthy-but-late peer must never trip it.  A latency-
+// critical caller (decode serving) may set a short bound per communicator
+// (xgmi_set_timeout); EMA_XGMI_TIMEOUT_MS overrides the default.
+int64_t default_timeout_ms() {
+  static const int64_t ms = [] {
+    const char* e = getenv("EMA_XGMI_TIMEOUT_MS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 60000);
+  }();
+  return ms;
+}
+
 struct XgComm {
   int rank = 0, world = 0, dev = 0;
   int64_t cap = 0, maxwg = 0;
+  int64_t timeout_ms = 0;           // peer-wait bound (default_timeout_ms())
   char* base = nullptr;             // own region
   std::vector<char*> peers;         // mapped peer regions (own at [rank])
   int64_t data_bytes() const { return 2 * (int64_t)world * cap; }
@@ -178,6 +193,7 @@ int64_t xgmi_create(int rank, int world, int64_t cap, void* handle_out) {
   c->world = world;
   c->cap = cap;
   c->maxwg = cap / XG_CHUNK;
+  c->timeout_ms = default_timeout_ms();
   hip_ok(hipGetDevice(&c->dev), "hipGetDevice");
   void* p = nullptr;
   hip_ok(hipExtMallocWithFlags(&p, (size_t)c->total(), hipDeviceMallocUncached), "uncached malloc");
@@ -210,14 +226,6 @@ void xgmi_open(int64_t id, const void* handles) {
 
 int64_t xgmi_capacity(int64_t id) { return get(id)->cap; }
 
-uint64_t timeout_ticks() {
-  static const uint64_t ticks = [] {
-    const char* e = getenv("EMA_XGMI_TIMEOUT_MS");
-    const long ms = e ? atol(e) : 1000;
-    return (uint64_t)(ms > 0 ? ms : 1000) * 100000ull;  // 100 MHz
-  }();
-  return ticks;
-}
 
 void xgmi_launch(int64_t id, const void* in, void* out, int64_t nbytes, int dt, bool gather,
                  hipStream_t s) {
@@ -240,7 +248,7 @@ void xgmi_launch(int64_t id, const void* in, void* out, int64_t nbytes, int dt, 
   a.cap = c->cap;
   a.rank = c->rank;
   a.world = c->world;
-  a.timeout_ticks = timeout_ticks();
+  a.timeout_ticks = (uint64_t)c->timeout_ms * 100000ull;  // s_memrealtime runs at 100 MHz
   if ((uintptr_t)in % 16 || (uintptr_t)out % 16)
     throw std::runtime_error("xgmi: input and output must be 16-B aligned (parallel/xgmi.py stages)");
   const unsigned grid = (unsigned)((nbytes + XG_CHUNK - 1) / XG_CHUNK);
@@ -261,6 +269,18 @@ void xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t nbytes, int 
 
 void xgmi_all_gather(int64_t id, const void* in, void* out, int64_t nbytes, int dt, hipStream_t s) {
   xgmi_launch(id, in, out, nbytes, dt, true, s);
+}
+
+void xgmi_set_timeout(int64_t id, int64_t ms) {
+  if (ms <= 0) throw std::runtime_error("xgmi: timeout must be positive");
+  get(id)->timeout_ms = ms;
+}
+
+int64_t xgmi_get_timeout(int64_t id) { return get(id)->timeout_ms; }
+
+void* xgmi_error_word(int64_t id) {
+  XgComm* c = get(id);
+  return c->base + c->error_off();
 }
 
 int xgmi_error(int64_t id) {

@@ -25,6 +25,11 @@ def get_args():
     return _get("args", "args")
 
 
+def get_args_or_none():
+    """The parsed args, or None outside an initialized run (library use)."""
+    return _G["args"]
+
+
 def get_num_microbatches():
     return _get("num_microbatches_calculator", "num microbatches calculator").get()
 

@@ -10,7 +10,7 @@ rank's pipeline (the reference did the same, :59-110).
 import torch
 import torch.distributed as dist
 
-from ..parallel import state
+from ..parallel import comm, state
 
 
 def device():
@@ -47,7 +47,7 @@ def broadcast_from_last_pipeline_stage(size, dtype, tensor=None):
     else:
         tensor = torch.empty(size, dtype=dtype, device=device())
     if state.get_pipeline_model_parallel_world_size() > 1:
-        dist.broadcast(tensor, state.get_pipeline_model_parallel_last_rank(),
+        comm.broadcast(tensor, state.get_pipeline_model_parallel_last_rank(),
                        group=state.get_pipeline_model_parallel_group())
     return tensor
 
@@ -64,7 +64,7 @@ def broadcast_from_last_to_first_pipeline_stage(size, dtype, tensor=None):
             raise AssertionError("tensor must be contiguous on the communication device")
     else:
         tensor = torch.empty(size, dtype=dtype, device=device())
-    dist.broadcast(tensor, state.get_pipeline_model_parallel_last_rank(),
+    comm.broadcast(tensor, state.get_pipeline_model_parallel_last_rank(),
                    group=state.get_embedding_group())
     return tensor
 
@@ -79,7 +79,7 @@ def copy_from_last_to_first_pipeline_stage(size, dtype, tensor=None):
     buf = tensor if tensor.is_contiguous() else torch.empty(size, dtype=dtype, device=device())
     if last and buf is not tensor:
         buf.copy_(tensor)
-    dist.broadcast(buf, state.get_pipeline_model_parallel_last_rank(),
+    comm.broadcast(buf, state.get_pipeline_model_parallel_last_rank(),
                    group=state.get_embedding_group())
     if first and buf is not tensor:
         tensor.copy_(buf)
@@ -92,7 +92,7 @@ def broadcast_tensor(size, dtype, tensor=None, rank=0):
             raise AssertionError("tensor must be contiguous on the communication device")
     else:
         tensor = torch.empty(size, dtype=dtype, device=device())
-    dist.broadcast(tensor, rank)
+    comm.broadcast(tensor, rank)
     return tensor
 
 

@@ -33,6 +33,8 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
         load_args_from_checkpoint(args)
     validate_args(args, args_defaults)
     global_vars.set_global_variables(args)
+    from .parallel.tensor import layers as _layers  # noqa: PLC0415
+    _layers.set_sp_keep_gathered(not getattr(args, "sp_regather_inputs", False))
     if getattr(args, "recompute_memory_budget_gb", None):
         resolve_recompute_budget(args)
     _initialize_distributed(args)
@@ -126,7 +128,7 @@ def _initialize_distributed(args):
         # the one-shot kernel needs GPU peer memory)
         from .parallel import comm
         comm.enable_xgmi_allreduce(state.get_tensor_model_parallel_group(), xg_kb * 1024,
-                                   ag_kb * 1024)
+                                   ag_kb * 1024, timeout_ms=getattr(args, "tp_xgmi_timeout_ms", None))
     if args.world_size > 1 and getattr(args, "comm_selfcheck", True):
         from .parallel.selfcheck import collective_selfcheck
         collective_selfcheck()

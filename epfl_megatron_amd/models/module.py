@@ -75,12 +75,13 @@ class MegatronModule(torch.nn.Module):
                 prm.shared = True
         if not dist.is_initialized():
             return
+        from ..parallel import comm  # noqa: PLC0415 (accounted, race-checked)
         if state.is_rank_in_embedding_group():
-            dist.all_reduce(self.word_embeddings_weight().data, group=state.get_embedding_group())
+            comm.all_reduce(self.word_embeddings_weight().data, group=state.get_embedding_group())
         if state.is_rank_in_position_embedding_group() and \
                 args.pipeline_model_parallel_split_rank is not None:
             pe = self.language_model.embedding.position_embeddings
-            dist.all_reduce(pe.weight.data, group=state.get_position_embedding_group())
+            comm.all_reduce(pe.weight.data, group=state.get_position_embedding_group())
 
 
 def _convert(val, fn):

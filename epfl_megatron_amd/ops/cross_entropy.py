@@ -14,9 +14,8 @@ with TP > 1 it is two passes around the RCCL all-reduces of ``[tokens]``
 vectors.  Label smoothing is supported on the reference (torch) path.
 """
 import torch
-import torch.distributed as dist
 
-from ..parallel import state
+from ..parallel import comm, state
 from ._ext import ext, use_native
 
 
@@ -26,8 +25,10 @@ def _vocab_range(part_vocab):
 
 
 def _tp_allreduce(t, op):
+    # through parallel/comm.py: accounted ("all_reduce/tp"), race-checked,
+    # looped back under the simulated-TP proxy, xGMI one-shot when registered
     if state.get_tensor_model_parallel_world_size() > 1:
-        dist.all_reduce(t, op=op, group=state.get_tensor_model_parallel_group())
+        comm.all_reduce(t, group=state.get_tensor_model_parallel_group(), op=op)
     return t
 
 
@@ -48,10 +49,10 @@ class _VocabParallelCEFn(torch.autograd.Function):
             loss, lse = ext().ce_fwd_fused(z, tgt)
         else:
             rmax = ext().ce_row_max(z)
-            _tp_allreduce(rmax, dist.ReduceOp.MAX)
+            _tp_allreduce(rmax, "max")
             sumexp, tlogit = ext().ce_sumexp_target(z, tgt, rmax, start)
-            _tp_allreduce(sumexp, dist.ReduceOp.SUM)
-            _tp_allreduce(tlogit, dist.ReduceOp.SUM)
+            _tp_allreduce(sumexp, "sum")
+            _tp_allreduce(tlogit, "sum")
             lse = torch.log(sumexp) + rmax
             loss = lse - tlogit
         ctx.save_for_backward(z, tgt, lse)
@@ -71,23 +72,23 @@ def _ce_ref(vocab_parallel_logits, target, label_smoothing=0.0):
     """fp32 torch math, TP-aware (three all-reduces like the reference)."""
     logits = vocab_parallel_logits.float()
     vmax = logits.max(dim=-1)[0]
-    _tp_allreduce(vmax, dist.ReduceOp.MAX)
+    _tp_allreduce(vmax, "max")
     logits = logits - vmax.unsqueeze(-1)
     part_v = logits.shape[-1]
     start, end = _vocab_range(part_v)
     mask = (target < start) | (target >= end)
     local_t = (target - start).masked_fill(mask, 0)
     pred = logits.gather(-1, local_t.unsqueeze(-1)).squeeze(-1).masked_fill(mask, 0.0)
-    _tp_allreduce(pred, dist.ReduceOp.SUM)
+    _tp_allreduce(pred, "sum")
     sum_exp = logits.exp().sum(dim=-1)
-    _tp_allreduce(sum_exp, dist.ReduceOp.SUM)
+    _tp_allreduce(sum_exp, "sum")
     loss = torch.log(sum_exp) - pred
     if label_smoothing > 0:
         vocab = part_v * state.get_tensor_model_parallel_world_size()
         smoothing = label_smoothing * vocab / (vocab - 1)
         log_probs = logits - torch.log(sum_exp).unsqueeze(-1)
         mean_lp = log_probs.sum(-1)
-        _tp_allreduce(mean_lp, dist.ReduceOp.SUM)
+        _tp_allreduce(mean_lp, "sum")
         mean_lp = mean_lp / vocab
         loss = (1.0 - smoothing) * loss - smoothing * mean_lp
     return loss
@@ -101,17 +102,17 @@ class _RefCEFn(torch.autograd.Function):
         with torch.no_grad():
             zf = logits.float()
             vmax = zf.max(dim=-1)[0]
-            _tp_allreduce(vmax, dist.ReduceOp.MAX)
+            _tp_allreduce(vmax, "max")
             zf = zf - vmax.unsqueeze(-1)
             part_v = zf.shape[-1]
             start, end = _vocab_range(part_v)
             mask = (target < start) | (target >= end)
             local_t = (target - start).masked_fill(mask, 0)
             pred = zf.gather(-1, local_t.unsqueeze(-1)).squeeze(-1).masked_fill(mask, 0.0)
-            _tp_allreduce(pred, dist.ReduceOp.SUM)
+            _tp_allreduce(pred, "sum")
             ez = zf.exp()
             sum_exp = ez.sum(-1)
-            _tp_allreduce(sum_exp, dist.ReduceOp.SUM)
+            _tp_allreduce(sum_exp, "sum")
             loss = torch.log(sum_exp) - pred
             softmax = ez / sum_exp.unsqueeze(-1)
             vocab = part_v * state.get_tensor_model_parallel_world_size()
@@ -119,7 +120,7 @@ class _RefCEFn(torch.autograd.Function):
                 smoothing = label_smoothing * vocab / (vocab - 1)
                 log_probs = torch.log(softmax.clamp_min(1e-30))
                 mean_lp = log_probs.sum(-1)
-                _tp_allreduce(mean_lp, dist.ReduceOp.SUM)
+                _tp_allreduce(mean_lp, "sum")
                 loss = (1.0 - smoothing) * loss - smoothing * (mean_lp / vocab)
             ctx.save_for_backward(softmax, mask, local_t)
             ctx.label_smoothing, ctx.vocab = label_smoothing, vocab

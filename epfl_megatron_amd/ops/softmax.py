@@ -3,10 +3,13 @@
 Reference kernels N1-N5 (``megatron/fused_kernels/scaled_*softmax*``) and the
 dispatcher ``FusedScaleMaskSoftmax`` (``megatron/model/fused_softmax.py``).
 On MI355X one HIP kernel family (``csrc/softmax.hip``) covers the three modes
-(causal upper-triangular, explicit padding mask, no mask): one row per wave64,
-the row held in registers (sk <= 8192, removing the reference's 2048/4096 caps,
-SURVEY D6), fp32 math, masked entries written as exact zeros, fully-masked
-rows -> 0.  Backward is ``scale * y * (dy - sum(dy * y))``.
+(causal upper-triangular, explicit padding mask, no mask): one wave64 per row
+for sk <= 1024 (four rows per workgroup, in-wave reductions), one 256-thread
+workgroup per row above, the row held in registers (sk <= 8192, removing the
+reference's 2048/4096 caps), 16-byte vector loads / stores, fp32
+math, masked entries written as exact zeros, fully-masked rows -> 0.  A
+``[1, 1, sq, sk]`` mask is read with batch stride 0 (never expanded).
+Backward is ``scale * y * (dy - sum(dy * y))``.
 """
 import torch
 
@@ -68,11 +71,12 @@ class FusedScaleMaskSoftmax(torch.nn.Module):
             if getattr(self.attn_mask_type, 'name', '') == 'causal':
                 return _SoftmaxFn.apply(x, None, scale, _MODE_CAUSAL)
             if mask is not None:
-                m = mask
-                if m.dtype != torch.bool:
-                    m = m.bool()
-                m = m.expand(x.shape[0], 1, x.shape[2], x.shape[3]).contiguous() \
-                    if m.shape[0] != x.shape[0] else m.contiguous()
+                m = mask if mask.dtype == torch.bool else mask.bool()
+                if m.dim() == 4 and m.shape[1] == 1 and m.shape[0] in (1, x.shape[0]) \
+                        and tuple(m.shape[2:]) == tuple(x.shape[2:]):
+                    # [b or 1, 1, sq, sk]: the kernel indexes a broadcast batch
+                    return _SoftmaxFn.apply(x, m.contiguous(), scale, _MODE_MASK)
+                m = m.expand(x.shape[0], 1, x.shape[2], x.shape[3]).contiguous()
                 return _SoftmaxFn.apply(x, m, scale, _MODE_MASK)
             return _SoftmaxFn.apply(x, None, scale, _MODE_NONE)
         return self.forward_torch_softmax(x, mask)

@@ -382,6 +382,7 @@ class MegatronOptimizer:
         for c in self.chunks:
             v = K.grad_norm_sq(c.ddp.grad_buffer, c.plan).reshape(1).float()
             tot = v if tot is None else tot + v
+        tot = comm.fold_xgmi_error(tot)  # a timed-out xGMI wait skips the step everywhere
         if dist.is_initialized():
             comm.all_reduce(tot, group=self._norm_group())
         return tot

@@ -6,17 +6,30 @@ activation for sequence-parallel GEMMs in a named, persistent scratch tensor
 avoids allocator fragmentation across the 288 GB pool and keeps the address
 stable for hipGraph capture.
 """
+import itertools
 import operator
 from functools import reduce
 
 import torch
 
+_GENERATIONS = itertools.count(1)  # process-wide: never reused across buffer objects
+
 
 class GlobalMemoryBuffer:
-    """Named scratch tensors, grown on demand and handed out as views."""
+    """Named scratch tensors, grown on demand and handed out as views.
+
+    Each buffer carries a *generation* that moves whenever the buffer is
+    (re)allocated or handed out with a different shape than the previous
+    request: two users of one name with different views (e.g. the SP forward's
+    ``[c, tp*R, h]`` pieces and the backward's ``[tp*rl, h]`` re-gather) then
+    never look like the same contents to code that caches facts about the
+    bytes (the simulated-TP loopback all-gather, ``parallel/comm.py``)."""
 
     def __init__(self):
         self._buffers = {}
+        self._last_shape = {}
+        self._gen = {}
+        self._by_ptr = {}  # storage data_ptr -> key
 
     def get_tensor(self, shape, dtype, name):
         numel = reduce(operator.mul, shape, 1)
@@ -24,9 +37,23 @@ class GlobalMemoryBuffer:
         buf = self._buffers.get(key)
         if buf is None or buf.numel() < numel:
             device = torch.cuda.current_device() if torch.cuda.is_available() else "cpu"
+            if buf is not None:
+                self._by_ptr.pop(buf.untyped_storage().data_ptr(), None)
             buf = torch.empty(numel, dtype=dtype, device=device, requires_grad=False)
             self._buffers[key] = buf
+            self._by_ptr[buf.untyped_storage().data_ptr()] = key
+            self._last_shape[key] = None
+        shape = tuple(shape)
+        if self._last_shape.get(key) != shape:
+            self._last_shape[key] = shape
+            self._gen[key] = next(_GENERATIONS)
         return buf[:numel].view(*shape)
+
+    def owner(self, t):
+        """``(key, generation)`` of the scratch buffer holding ``t``, or None
+        (one dict lookup by storage address)."""
+        key = self._by_ptr.get(t.untyped_storage().data_ptr())
+        return None if key is None else (key, self._gen[key])
 
 
 _GLOBAL_BUFFER = None

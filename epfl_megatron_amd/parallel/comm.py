@@ -26,7 +26,6 @@ Two debug/observability aids live here:
   gradients; the CPU tests run with the checker on.
 """
 import os
-import weakref
 import time
 from collections import OrderedDict
 
@@ -78,7 +77,7 @@ def set_loopback(group, world):
         _GROUP_SIZES[name] = int(world)
 
 
-def enable_xgmi_allreduce(group, cap_bytes, gather_cap_bytes=None):
+def enable_xgmi_allreduce(group, cap_bytes, gather_cap_bytes=None, timeout_ms=None):
     """Route sum all-reduces of at most ``cap_bytes`` and all-gathers of at
     most ``gather_cap_bytes`` per rank (default: ``cap_bytes``) on ``group``
     (contiguous bf16 / fp16 / fp32 CUDA tensors) through the one-shot xGMI
@@ -90,8 +89,21 @@ def enable_xgmi_allreduce(group, cap_bytes, gather_cap_bytes=None):
     ag = cap_bytes if gather_cap_bytes is None else gather_cap_bytes
     if cap_bytes or ag:
         from .xgmi import XgmiAllReduce  # noqa: PLC0415
-        _XGMI[id(group)] = XgmiAllReduce(group, cap_bytes or 0, ag or 0)
+        _XGMI[id(group)] = XgmiAllReduce(group, cap_bytes or 0, ag or 0, timeout_ms=timeout_ms)
     return _XGMI.get(id(group))
+
+
+def fold_xgmi_error(t):
+    """``t`` (a float tensor on the device, e.g. the local grad-norm square)
+    turned to +inf where any registered one-shot collective has timed out, so
+    the non-finite-norm skip drops the step on every rank after the norm's
+    all-reduce, with no host sync (NaN-poisoned activations must
+    never reach the weights)."""
+    for xg in _XGMI.values():
+        err = xg.error_tensor()
+        if err is not None and err.device == t.device:
+            t = torch.where(err.to(t.dtype) != 0, torch.full_like(t, float("inf")), t)
+    return t
 
 
 def check_xgmi():
@@ -249,21 +261,15 @@ _LOOP_STREAMS = {}
 # (profiles/r5x_loopback_stream_ab.txt).
 _LOOP_SIDE_STREAM = os.environ.get("EMA_LOOPBACK_STREAM", "0") == "1"
 # Simulated peers' slots of a loopback all-gather into a persistent scratch
-# buffer (parallel/buffers.py) are written once per (buffer, range): they then
-# hold finite activations for good, and the per-call traffic is this rank's
-# own slot, as the proxy's compute-only accounting assumes.  Any other output
-# (a fresh allocation that may hold recycled bytes) is fully written each call.
-_LOOP_FILLED = {}  # id(scratch buffer) -> filled (offset, numel); dropped with the buffer
-
-
-def _scratch_owner(t):
-    """The live GlobalMemoryBuffer tensor holding ``t`` (None: not scratch)."""
-    from .buffers import get_global_memory_buffer
-    ptr = t.untyped_storage().data_ptr()
-    for buf in get_global_memory_buffer()._buffers.values():
-        if buf.untyped_storage().data_ptr() == ptr:
-            return buf
-    return None
+# buffer (parallel/buffers.py) are written once per (buffer, generation,
+# range): between two hand-outs of the buffer with the same view nothing else
+# writes it, so the slots still hold the finite activations written then, and
+# the per-call traffic is this rank's own slot, as the proxy's compute-only
+# accounting assumes.  A new generation (the buffer re-allocated, or handed out
+# with another shape, i.e. possibly written by another user) refills them.
+# Any other output (a fresh allocation that may hold recycled bytes) is fully
+# written each call.  Proxy-only: a real all-gather writes every slot anyway.
+_LOOP_FILLED = set()  # (buffer key, generation, storage offset, numel)
 
 
 def _loop_async(fn, tensors):
@@ -375,20 +381,18 @@ def all_gather_into(output, inp, group=None, async_op=False):
             # compute as RCCL's would, with a real rank's write traffic
             rows = output.view(n, -1)
             flat = src.reshape(1, -1)
-            owner = _scratch_owner(output)
-            key = (output.storage_offset(), output.numel())
-            if owner is not None and id(owner) not in _LOOP_FILLED:
-                _LOOP_FILLED[id(owner)] = set()
-                weakref.finalize(owner, _LOOP_FILLED.pop, id(owner), None)
-            peers = owner is None or key not in _LOOP_FILLED[id(owner)]
+            from .buffers import get_global_memory_buffer  # noqa: PLC0415
+            owner = get_global_memory_buffer().owner(output)
+            key = None if owner is None else owner + (output.storage_offset(), output.numel())
+            peers = key is None or key not in _LOOP_FILLED
 
             def fill():
                 if rows[0].data_ptr() != src.data_ptr():
                     rows[0:1].copy_(flat)
                 if peers:
                     rows[1:].copy_(flat.expand(n - 1, -1))
-            if owner is not None:
-                _LOOP_FILLED[id(owner)].add(key)
+            if key is not None:
+                _LOOP_FILLED.add(key)
             return _loop_async(fill, [output, src])
         return _issue("all_gather", group, output, src, loop, async_op)
     xg = _XGMI.get(id(group))

@@ -17,10 +17,65 @@ REAL backend and compares the results with values it can compute locally:
 Any mismatch raises ``RuntimeError`` naming the group and the operation
 before any model memory is allocated.  Cost: ~20 collectives of <= 1 KiB.
 Reference: the reference had no such check (``megatron/initialize.py:124-159``).
+
+Environment knobs.  ``EMA_*`` variables are read at import time, and several
+change how many collectives a step posts, or their shapes (``EMA_SP_CHUNKS``,
+``EMA_SP_MLP_PIECES``, ``EMA_FUSED_MLP``, ``EMA_NT_GEMM``, ``EMA_COMM_CHECK``,
+...).  A rank started with a different value would post a different sequence
+and hang RCCL mid-step, so :func:`check_env_agrees` all-gathers a hash of every
+``EMA_*`` variable that is not known to be rank-local (kernel tuning, tracing)
+and refuses to start on a mismatch, naming the differing variables.
 """
+import hashlib
+import json
+import os
+
 import torch
+import torch.distributed as dist
 
 from . import comm, state
+
+# EMA_* variables that only tune a kernel's schedule or a rank-local aid; they
+# may differ between ranks.  Every other EMA_* variable is treated as able to
+# change the collective sequence (conservative: a new knob is checked unless
+# it is listed here).
+_LOCAL_KNOBS = ("EMA_TRACE", "EMA_STRICT_KERNELS", "EMA_OFFLOAD_ARCH", "EMA_EMBEDDED",
+                "EMA_XGMI_TIMEOUT_MS", "EMA_LOOPBACK_STREAM", "EMA_DGRAD_WT",
+                "EMA_NORM_MAIN_GRAD", "EMA_SKINNY_PACK", "EMA_SKINNY_WAVES",
+                "EMA_SKINNY_PERSIST", "EMA_WGRAD_MIN_TILES")
+_LOCAL_PREFIXES = ("EMA_GEMM_", "EMA_WGRAD_", "EMA_FA_", "EMA_RMS_")
+
+
+def structural_env(environ=None):
+    """The ``EMA_*`` variables that must agree across ranks (sorted dict)."""
+    environ = os.environ if environ is None else environ
+    return {k: environ[k] for k in sorted(environ)
+            if k.startswith("EMA_") and k not in _LOCAL_KNOBS
+            and not k.startswith(_LOCAL_PREFIXES)}
+
+
+def check_env_agrees(environ=None):
+    """All-gather a hash of :func:`structural_env` over the world; raise
+    ``RuntimeError`` naming the variables whose values differ.  Returns the
+    number of ranks compared (1: nothing to do)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return 1
+    env = structural_env(environ)
+    digest = hashlib.sha256(json.dumps(env, sort_keys=True).encode()).digest()
+    mine = torch.tensor([int.from_bytes(digest[:7], "little")], dtype=torch.int64, device=_dev())
+    world = dist.get_world_size()
+    every = torch.empty(world, dtype=torch.int64, device=_dev())
+    comm.all_gather_into(every, mine)
+    if bool((every == every[0]).all()):
+        return world
+    envs = [None] * world  # the slow path names the culprits (host objects)
+    dist.all_gather_object(envs, env)
+    keys = sorted(set().union(*envs))
+    diff = {k: [e.get(k) for e in envs] for k in keys if len({e.get(k) for e in envs}) > 1}
+    raise RuntimeError(
+        "EMA_* environment differs between ranks; these variables change the collective "
+        "sequence and must be identical on every rank (value per rank, None = unset): "
+        + "; ".join(f"{k}={v}" for k, v in diff.items()))
 
 
 def _dev():
@@ -98,7 +153,7 @@ def _check_pipeline(dev):
 def collective_selfcheck(verbose=True):
     """Run the checks on every group this rank belongs to; returns the count."""
     dev = _dev()
-    n = 0
+    n = 1 if check_env_agrees() > 1 else 0
     dp_groups = state.get_data_parallel_comm_groups()
     for i, g in enumerate(dp_groups):
         n += _check_group(f"dp[{i}]", g, state.get_data_parallel_world_size(),

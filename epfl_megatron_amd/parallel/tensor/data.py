@@ -7,11 +7,18 @@ Host->device: the flat payload is staged in a small ring of pinned host
 buffers and copied with ``non_blocking=True``, so feeding a micro-batch never
 blocks the host on the GPU queue.  Without TP there is nothing to broadcast and
 the sizes come straight from the host tensors (no size round trip).
+
+Under TP the receiving ranks need the shapes on the HOST to size the payload,
+and reading a broadcast size vector back drains the GPU queue.  So the sizes
+are broadcast once per key set and then reused (every micro-batch of a run has
+the same shapes); only ``--variable_seq_lengths`` re-broadcasts them each call.
+TP-rank 0 checks its real shapes against the cached ones and raises rather
+than let the group post mismatched broadcasts.  Both broadcasts go through
+``parallel/comm.py`` (accounted as ``broadcast/tp``).
 """
 import torch
-import torch.distributed as dist
 
-from .. import state
+from .. import comm, state
 
 _MAX_DATA_DIM = 5
 
@@ -64,9 +71,9 @@ def _build_key_size_numel_dictionaries(keys, data):
                 sizes[i * _MAX_DATA_DIM + j] = d
     sizes_t = torch.tensor(sizes, dtype=torch.long, device=_device())
     if state.get_tensor_model_parallel_world_size() > 1:
-        dist.broadcast(sizes_t, state.get_tensor_model_parallel_src_rank(),
+        comm.broadcast(sizes_t, state.get_tensor_model_parallel_src_rank(),
                        group=state.get_tensor_model_parallel_group())
-    sizes_cpu = sizes_t.cpu().tolist()
+    sizes_cpu = sizes_t.cpu().tolist()  # the one host sync (first call per key set)
     key_size, key_numel, total = {}, {}, 0
     for i, key in enumerate(keys):
         shape = []
@@ -97,11 +104,35 @@ def _local_sizes(keys, data):
     return key_size, key_numel, total
 
 
+_SIZE_CACHE = {}  # (tuple(keys), id(tp group)) -> (key_size, key_numel, total)
+
+
+def _variable_lengths():
+    from ...global_vars import get_args_or_none
+    args = get_args_or_none()
+    return bool(getattr(args, "variable_seq_lengths", False))
+
+
+def reset_size_cache():
+    _SIZE_CACHE.clear()
+
+
 def broadcast_data(keys, data, datatype):
     if state.get_tensor_model_parallel_world_size() == 1:
         key_size, key_numel, total = _local_sizes(keys, data)
     else:
-        key_size, key_numel, total = _build_key_size_numel_dictionaries(keys, data)
+        ck = (tuple(keys), id(state.get_tensor_model_parallel_group()))
+        hit = None if _variable_lengths() else _SIZE_CACHE.get(ck)
+        if hit is None:
+            hit = _SIZE_CACHE[ck] = _build_key_size_numel_dictionaries(keys, data)
+        elif state.get_tensor_model_parallel_rank() == 0:
+            for key in keys:
+                if list(data[key].size()) != hit[0][key]:
+                    raise RuntimeError(
+                        f"broadcast_data: '{key}' has shape {list(data[key].size())} but this "
+                        f"run's batches had {hit[0][key]}; shapes are broadcast once per run "
+                        "unless --variable_seq_lengths is set")
+        key_size, key_numel, total = hit
     if state.get_tensor_model_parallel_rank() == 0:
         for key in keys:
             if data[key].dtype != datatype:
@@ -112,7 +143,7 @@ def broadcast_data(keys, data, datatype):
     else:
         flat = torch.empty(total, device=_device(), dtype=datatype)
     if state.get_tensor_model_parallel_world_size() > 1:
-        dist.broadcast(flat, state.get_tensor_model_parallel_src_rank(),
+        comm.broadcast(flat, state.get_tensor_model_parallel_src_rank(),
                        group=state.get_tensor_model_parallel_group())
     out, offset = {}, 0
     for key in keys:

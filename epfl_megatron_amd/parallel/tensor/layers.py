@@ -215,7 +215,7 @@ def _weight_t(weight):
     return wt
 
 
-def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
+def _wgrad_into_main_grad(weight, grad_output_2d, input_2d, x_map=None):
     """main_grad[out, in] (+)= dY^T @ X with fp32 accumulation, in place.
 
     ``weight._mg_fresh`` (set by ``DistributedDataParallel.zero_grad_buffer``
@@ -233,12 +233,16 @@ def _wgrad_into_main_grad(weight, grad_output_2d, input_2d):
         K = input_2d.shape[1]
         if _WGRAD_KERNEL and main_grad.is_contiguous() and grad_output_2d.is_contiguous() \
                 and input_2d.is_contiguous() and ext().wgrad_supported(M, N, K) \
-                and (-(-N // 256)) * (-(-K // 256)) >= _WGRAD_MIN_TILES:
-            ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate)
+                and (-(-N // 256)) * (-(-K // 256)) >= _WGRAD_MIN_TILES \
+                and (x_map is None or x_map[0] % 32 == 0):
+            ext().wgrad_gemm(grad_output_2d, input_2d, main_grad.view(N, K), accumulate,
+                             list(x_map) if x_map is not None else [])
         else:
-            torch.addmm(main_grad, grad_output_2d.t(), input_2d, beta=1.0 if accumulate else 0.0,
-                        out_dtype=torch.float32, out=main_grad)
-    elif accumulate:
+            torch.addmm(main_grad, grad_output_2d.t(), _apply_token_map(input_2d, x_map, M),
+                        beta=1.0 if accumulate else 0.0, out_dtype=torch.float32, out=main_grad)
+        return
+    input_2d = _apply_token_map(input_2d, x_map, grad_output_2d.shape[0])
+    if accumulate:
         main_grad.addmm_(grad_output_2d.t().to(main_grad.dtype), input_2d.to(main_grad.dtype))
     else:
         torch.mm(grad_output_2d.t().to(main_grad.dtype), input_2d.to(main_grad.dtype),
@@ -365,6 +369,24 @@ def gemm_dglu(g, w2t, pre, kind, out=None):
 # blocking forms).
 _SP_CHUNKS = int(os.environ.get("EMA_SP_CHUNKS", "2"))
 
+# Keep the forward's all-gathered SP inputs of the column-parallel products
+# (QKV, fc1, the LM head) for their weight gradients instead of all-gathering
+# them again in the backward (the reference re-gathers: megatron/core/
+# tensor_parallel/layers.py:250-262).  That removes 2 of the 10 full-size
+# [s, b, h] TP collectives per layer and micro-batch for [s, b, h] bf16 of
+# HBM per product while the layer's activations live (charged by
+# utils/memory_model.py).  Under full recompute the recompute forward's
+# gathers are the ones kept.  --sp_regather_inputs restores the re-gather.
+_SP_KEEP_GATHERED = [True]
+
+
+def set_sp_keep_gathered(flag):
+    _SP_KEEP_GATHERED[0] = bool(flag)
+
+
+def sp_keep_gathered():
+    return _SP_KEEP_GATHERED[0]
+
 
 def _sp_pieces(rows_local):
     c = max(1, _SP_CHUNKS)
@@ -376,9 +398,11 @@ def _tp():
     return world, (state.get_tensor_model_parallel_group() if world > 1 else None)
 
 
-def sp_allgather_gemm(x_local, w, glu_kind=None):
+def sp_allgather_gemm(x_local, w, glu_kind=None, keep=False):
     """Column-parallel forward under SP: AG(x_local) @ w^T (or the fused GLU
-    pair) with the all-gather pipelined against the GEMM.  x_local [rl, K]."""
+    pair) with the all-gather pipelined against the GEMM.  x_local [rl, K].
+    ``keep``: gather into a fresh tensor and return it too (piece-major
+    ``[c, tp * R, K]``; ``gathered_token_map`` pairs it with natural rows)."""
     world, group = _tp()
     rl, K = x_local.shape
     c = _sp_pieces(rl)
@@ -390,7 +414,10 @@ def sp_allgather_gemm(x_local, w, glu_kind=None):
     else:
         pre = torch.empty(world * rl, 2 * n, dtype=dt, device=dev)
         y = torch.empty(world * rl, n, dtype=dt, device=dev)
-    g = get_global_memory_buffer().get_tensor((c, world * R, K), dt, "mpu")
+    if keep:
+        g = torch.empty((c, world * R, K), dtype=dt, device=dev)
+    else:
+        g = get_global_memory_buffer().get_tensor((c, world * R, K), dt, "mpu")
     works = [comm.all_gather_into(g[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
              for j in range(c)]
     for j in range(c):
@@ -400,7 +427,31 @@ def sp_allgather_gemm(x_local, w, glu_kind=None):
             gemm(g[j], w, out, c_map=cmap)
         else:
             gemm_glu(g[j], w, glu_kind, pre, y, c_map=cmap)
-    return out if glu_kind is None else (pre, y)
+    res = out if glu_kind is None else (pre, y)
+    return (res, g) if keep else res
+
+
+def gathered_token_map(rl, world):
+    """Token map (``wgrad_gemm``'s x_map) from natural rows ``[rank][rl]`` of a
+    sequence-parallel product to the piece-major rows ``[piece][rank][R]`` of
+    ``sp_allgather_gemm``'s gather: natural q = (r, j, i) -> j * world * R +
+    r * R + i.  None when the gather is in natural order (one piece)."""
+    c = _sp_pieces(rl)
+    if c == 1:
+        return None
+    R = rl // c
+    return (R, c, world * R, R)
+
+
+def _apply_token_map(x2, x_map, m):
+    """X rows in dY's token order (the torch form of the kernel's x_map)."""
+    if x_map is None:
+        return x2
+    R, n1, s1, s2 = x_map
+    q = torch.arange(m, device=x2.device)
+    grp = q // R
+    idx = (grp % n1) * s1 + (grp // n1) * s2 + (q - grp * R)
+    return x2.index_select(0, idx)
 
 
 def sp_gemm_reducescatter(x_full, w):
@@ -447,15 +498,21 @@ def _fwd(x2, weight):
 _NT_GEMM = os.environ.get("EMA_NT_GEMM", "0") == "1"
 
 
-def _linear_backward(input_, weight, grad_output, use_bias, gaf, async_ar, sp):
+def _linear_backward(input_, weight, grad_output, use_bias, gaf, async_ar, sp, kept=None):
     """Backward of Y = X W^T (+ b) for one TP rank.  ``sp``: ``input_`` is the
     local SP shard (re-gathered here, overlapped with the dgrad GEMM) and dX is
     reduce-scattered (overlapped with the wgrad GEMM); ``async_ar``: dX is
-    TP-all-reduced, overlapped with the wgrad GEMM."""
+    TP-all-reduced, overlapped with the wgrad GEMM.  ``kept``: the forward's
+    gathered input (``sp_allgather_gemm(keep=True)``) with its token map; no
+    re-gather (``input_`` then only gives the local shape)."""
     world, group = _tp()
     tp_group = group if world > 1 else None
     gather_handle = None
-    if sp:
+    x_map = None
+    if kept is not None:
+        gathered, x_map = kept
+        total = gathered.view(-1, gathered.shape[-1])
+    elif sp:
         shape = (input_.shape[0] * world,) + tuple(input_.shape[1:])
         total = get_global_memory_buffer().get_tensor(shape, input_.dtype, "mpu")
         gather_handle = comm.all_gather_into(total, input_, group=tp_group, async_op=True)
@@ -474,10 +531,10 @@ def _linear_backward(input_, weight, grad_output, use_bias, gaf, async_ar, sp):
     if sp:
         if async_ar:
             raise AssertionError("sequence parallel and async all-reduce are exclusive")
-        sub = torch.empty_like(input_)
+        sub = torch.empty(input_.shape, dtype=grad_input.dtype, device=grad_input.device)
         handle = comm.reduce_scatter_into(sub, grad_input, group=tp_group, async_op=True)
         grad_input = sub
-    grad_weight = _wgrad(weight, go2, ti2, gaf)
+    grad_weight = _wgrad(weight, go2, ti2, gaf, x_map)
     grad_bias = go2.sum(dim=0) if use_bias else None
     if handle is not None:
         handle.wait()
@@ -491,22 +548,31 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input_, weight, bias, gradient_accumulation_fusion,
                 async_grad_allreduce, sequence_parallel):
-        ctx.save_for_backward(input_, weight)
         ctx.use_bias = bias is not None
         ctx.gradient_accumulation_fusion = gradient_accumulation_fusion
         ctx.async_grad_allreduce = async_grad_allreduce
         ctx.sequence_parallel = sequence_parallel
+        ctx.kept_map = None
         K = input_.shape[-1]
         x2 = input_.reshape(-1, K)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
+        keep = sequence_parallel and sp_keep_gathered()
+        ctx.keep = keep
         if sequence_parallel:
             world = state.get_tensor_model_parallel_world_size()
-            out = sp_allgather_gemm(x2, weight)
+            out = sp_allgather_gemm(x2, weight, keep=keep)
+            if keep:
+                out, gathered = out
+                ctx.input_shape = tuple(input_.shape)
+                ctx.kept_map = gathered_token_map(x2.shape[0], world)
+                ctx.save_for_backward(gathered, weight)
             lead = (input_.shape[0] * world,) + tuple(input_.shape[1:-1])
         else:
             out = _fwd(x2, weight)
             lead = tuple(input_.shape[:-1])
+        if not keep:
+            ctx.save_for_backward(input_, weight)
         out = out.view(*lead, weight.shape[0])
         if bias is not None:
             out = out + bias
@@ -514,6 +580,14 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_output):
+        if ctx.keep:
+            gathered, weight = ctx.saved_tensors
+            shape_src = torch.empty(ctx.input_shape, dtype=gathered.dtype, device="meta")
+            gi, gw, gb = _linear_backward(shape_src, weight, grad_output, ctx.use_bias,
+                                          ctx.gradient_accumulation_fusion,
+                                          ctx.async_grad_allreduce, True,
+                                          kept=(gathered, ctx.kept_map))
+            return gi, gw, gb, None, None, None
         input_, weight = ctx.saved_tensors
         gi, gw, gb = _linear_backward(input_, weight, grad_output, ctx.use_bias,
                                       ctx.gradient_accumulation_fusion,
@@ -566,8 +640,12 @@ class _RowParallelSPFn(torch.autograd.Function):
         for j in range(c):
             works[j].wait()
             gemm(g[j], wt, gi, c_map=(R, c * R, j * R))
-        xp = x2.view(world, c, R, K).transpose(0, 1).reshape(c * world * R, K)
-        gw = _wgrad(weight, g.view(-1, H), xp, ctx.gaf)
+        # dY rows are piece-major ([piece][rank][R]); X stays in natural order
+        # and the wgrad reads it through a token map (no permutation copy):
+        # piece-major p = (j, r, i) -> natural r * c * R + j * R + i
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        gw = _wgrad(weight, g.view(-1, H), x2, ctx.gaf, (R, world, c * R, R))
         return gi.view(*input_.shape), gw, None
 
 
@@ -617,14 +695,18 @@ class _GluMLPFn(torch.autograd.Function):
         x2 = input_.reshape(-1, H)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
+        kept = None
         if sequence_parallel:
-            pre, y, out = _sp_mlp_forward(x2, w1, w2, kind)
+            pre, y, out, kept = _sp_mlp_forward(x2, w1, w2, kind)
             lead = tuple(input_.shape[:-1])
         else:
             pre, y = gemm_glu(x2, w1, kind)
             out = gemm(y, w2)
             lead = tuple(input_.shape[:-1])
-        ctx.save_for_backward(input_, w1, w2, pre, y)
+        ctx.kept = kept is not None
+        ctx.input_shape = tuple(input_.shape)
+        # with a kept gather the local input is not needed (shape only)
+        ctx.save_for_backward(kept if kept is not None else input_, w1, w2, pre, y)
         ctx.kind, ctx.sp, ctx.tp_async, ctx.gaf = kind, sequence_parallel, tp_async_allreduce, gaf
         ctx.world = world
         return out.view(*lead, w2.shape[0])
@@ -638,8 +720,13 @@ class _GluMLPFn(torch.autograd.Function):
         if not g2.is_contiguous():
             g2 = g2.contiguous()
         if ctx.sp:
-            dx, gw1, gw2 = _sp_mlp_backward(input_, g2, w1, w2, pre, y, ctx.kind, ctx.gaf)
-            return dx.view(*input_.shape), gw1, gw2, None, None, None, None
+            kept = None
+            if ctx.kept:
+                kept, input_ = input_, torch.empty(ctx.input_shape, dtype=input_.dtype,
+                                                   device="meta")
+            dx, gw1, gw2 = _sp_mlp_backward(input_, g2, w1, w2, pre, y, ctx.kind, ctx.gaf,
+                                            kept=kept)
+            return dx.view(*ctx.input_shape), gw1, gw2, None, None, None, None
         gather_handle = None
         total = input_
         # fc2 dgrad with the GLU backward in the epilogue: d(pre-act) [M, 2F]
@@ -696,8 +783,12 @@ def _sp_mlp_forward(x_local, w1, w2, kind):
     F = w2.shape[1]
     sizes = _sp_mlp_pieces(rl, world, 2 * F)
     offs = [sum(sizes[:j]) for j in range(len(sizes))]
-    # piece-major buffers: piece j's gathered rows at [world * off_j, world * (off_j + R_j))
-    g = get_global_memory_buffer().get_tensor((world * rl, H), dt, "mpu")
+    # piece-major buffers: piece j's gathered rows at [world * off_j, world * (off_j + R_j));
+    # kept for the fc1 wgrad (same piece order as every other MLP tensor)
+    if sp_keep_gathered():
+        g = torch.empty(world * rl, H, dtype=dt, device=dev)
+    else:
+        g = get_global_memory_buffer().get_tensor((world * rl, H), dt, "mpu")
     gp = [g[world * o:world * (o + r)] for o, r in zip(offs, sizes)]
     works = [comm.all_gather_into(gp[j], x_local[o:o + r], group=group, async_op=True)
              for j, (o, r) in enumerate(zip(offs, sizes))]
@@ -715,20 +806,20 @@ def _sp_mlp_forward(x_local, w1, w2, kind):
                                            async_op=True))
     for w in rs:
         w.wait()
-    return pre, y, out
+    return pre, y, out, (g if sp_keep_gathered() else None)
 
 
-def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf):
+def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf, kept=None):
     """Backward of ``_sp_mlp_forward``: dOut and X gathered in the forward's
     pieces; per piece the fc2 dgrad (+ GLU backward) and the fc1 dgrad run while
     the next piece's gathers fly, and dX's reduce-scatter of piece j overlaps
     piece j+1; both wgrads run last over all pieces."""
     world, group = _tp()
     x_local = input_.reshape(-1, input_.shape[-1])
-    if not x_local.is_contiguous():
+    if kept is None and not x_local.is_contiguous():
         x_local = x_local.contiguous()
     rl, H = x_local.shape
-    dt, dev = x_local.dtype, x_local.device
+    dt, dev = g_local.dtype, g_local.device
     F = w2.shape[1]
     sizes = _sp_mlp_pieces(rl, world, 2 * F)
     offs = [sum(sizes[:j]) for j in range(len(sizes))]
@@ -737,9 +828,12 @@ def _sp_mlp_backward(input_, g_local, w1, w2, pre, y, kind, gaf):
     g2 = buf.get_tensor((world * rl, g_local.shape[1]), g_local.dtype, "mpu_dy")
     gw = [comm.all_gather_into(g2[world * o:world * (o + r)], g_local[o:o + r], group=group,
                                async_op=True) for o, r in pieces]
-    xt = buf.get_tensor((world * rl, H), dt, "mpu")
-    xw = [comm.all_gather_into(xt[world * o:world * (o + r)], x_local[o:o + r], group=group,
-                               async_op=True) for o, r in pieces]
+    if kept is not None:  # the forward's gather (piece-major, as the re-gather would be)
+        xt, xw = kept, []
+    else:
+        xt = buf.get_tensor((world * rl, H), dt, "mpu")
+        xw = [comm.all_gather_into(xt[world * o:world * (o + r)], x_local[o:o + r], group=group,
+                                   async_op=True) for o, r in pieces]
     dpre = torch.empty(world * rl, 2 * F, dtype=dt, device=dev)
     dxp = torch.empty(world * rl, H, dtype=dt, device=dev)
     dx = torch.empty(rl, H, dtype=dt, device=dev)
@@ -768,13 +862,15 @@ def _weight_t_always(weight):
     return _transpose(weight) if _tn_ok(weight) else weight.t().contiguous()
 
 
-def _wgrad(weight, g2, x2, gaf):
-    """Weight gradient of Y = X W^T: into main_grad (returns None) or as a tensor."""
+def _wgrad(weight, g2, x2, gaf, x_map=None):
+    """Weight gradient of Y = X W^T: into main_grad (returns None) or as a
+    tensor.  ``x_map``: X's rows are a token permutation of dY's
+    (``wgrad_gemm``'s x_map, e.g. ``gathered_token_map``)."""
     if gaf and hasattr(weight, "main_grad"):
-        _wgrad_into_main_grad(weight, g2, x2)
+        _wgrad_into_main_grad(weight, g2, x2, x_map)
         _notify_grad_ready(weight)
         return None
-    return g2.t().matmul(x2)
+    return g2.t().matmul(_apply_token_map(x2, x_map, g2.shape[0]))
 
 
 def glu_mlp(input_, w1, w2, glu_kind, *, sequence_parallel, tp_async_allreduce,

@@ -30,10 +30,16 @@ would hang or time out).  All-reduces and all-gathers have separate caps
 (``--tp_xgmi_allreduce_kb`` / ``--tp_xgmi_allgather_kb``): the all-gather cap
 covers the multi-MiB sequence-parallel ``[s/tp, b, h]`` pieces.
 
-A wait on a peer is bounded by wall clock (``EMA_XGMI_TIMEOUT_MS``, default
-1000): a dead peer ends the kernel with NaN-filled output and the error word
-set, and :meth:`check` (called by every training log line and after every
-generate call) raises.
+A wait on a peer is bounded by wall clock: ``timeout_ms`` per communicator
+(default 60 s, or ``EMA_XGMI_TIMEOUT_MS``; ``--tp_xgmi_timeout_ms`` in
+training).  The bound is long on purpose: TP ranks drift apart through host
+work (checkpoint writes, first-iteration setup, a GC pause), and a late but
+healthy peer must not trip it; a latency-critical caller (decode serving) can
+pass a short one.  A dead peer ends the kernel with NaN-filled output and the
+device error word set.  The optimizer folds that word into the grad-norm
+reduction (:meth:`error_tensor`, ``comm.fold_xgmi_error``): every rank then
+skips the step on device, with no host sync; :meth:`check` (every training log
+line, the start of ``save_checkpoint``, after every generate call) raises.
 
 Verified on one MI355X with 2 and 4 processes sharing the GPU
 (``tests/test_xgmi_gpu.py``: same-device IPC mappings; the flag / parity
@@ -60,7 +66,7 @@ class XgmiAllReduce:
 
     DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
-    def __init__(self, group=None, cap_bytes=1 << 20, gather_cap_bytes=None):
+    def __init__(self, group=None, cap_bytes=1 << 20, gather_cap_bytes=None, timeout_ms=None):
         ar = int(cap_bytes)
         ag = ar if gather_cap_bytes is None else int(gather_cap_bytes)
         cap = max(ar, ag)
@@ -80,6 +86,10 @@ class XgmiAllReduce:
         dist.all_gather_object(handles, bytes(handle.numpy().tobytes()), group=group)
         table = torch.frombuffer(bytearray(b"".join(handles)), dtype=torch.uint8)
         C.xgmi_open(self.id, table.view(self.world, -1))
+        if timeout_ms is not None:
+            C.xgmi_set_timeout(self.id, int(timeout_ms))
+        self.timeout_ms = C.xgmi_get_timeout(self.id)
+        self._err = C.xgmi_error_tensor(self.id)
         dist.barrier(group=group)
 
     def _fits(self, t, cap):
@@ -131,6 +141,10 @@ class XgmiAllReduce:
             out.copy_(o)
         return out
 
+    def error_tensor(self):
+        """Device int32 [1]: nonzero once a peer wait has timed out."""
+        return self._err
+
     def check(self):
         """Raise if a wait timed out (a peer never arrived); synchronises."""
         if _ext().xgmi_error(self.id):
@@ -138,6 +152,7 @@ class XgmiAllReduce:
                             "bound; results since then are invalid")
 
     def close(self):
+        self._err = None
         if self.id is not None:
             _ext().xgmi_destroy(self.id)
             self.id = None

@@ -52,7 +52,7 @@ def pretrain(args, train_valid_test_dataset_provider, model_provider_func, model
     global _TRAIN_START_TIME
     t = torch.tensor([_TRAIN_START_TIME], dtype=torch.float64,
                      device=_device() if args.distributed_backend != "gloo" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    comm.all_reduce(t, op=dist.ReduceOp.MIN)
     _TRAIN_START_TIME = t.item()
     print_rank_0(f"time to initialize megatron (seconds): {time.time() - _TRAIN_START_TIME:.3f}")
     print_datetime("after megatron is initialized")
@@ -483,7 +483,7 @@ def _train(args, forward_step_func, model, optimizer, opt_param_scheduler, train
             train_time = (time.time() - _TRAIN_START_TIME) / 60.0
             done = torch.tensor([int(train_time > args.exit_duration_in_mins)],
                                 device=_device() if args.distributed_backend != "gloo" else "cpu")
-            dist.all_reduce(done, op=dist.ReduceOp.MAX)
+            comm.all_reduce(done, op="max")
             if done.item():
                 flush_log()
                 if not saved:
@@ -602,7 +602,7 @@ def build_train_valid_test_data_iterators(build_train_valid_test_datasets_provid
     else:
         flags = torch.zeros(3, dtype=torch.long, device=dev)
     if state.get_tensor_model_parallel_world_size() > 1:
-        dist.broadcast(flags, state.get_tensor_model_parallel_src_rank(),
+        comm.broadcast(flags, state.get_tensor_model_parallel_src_rank(),
                        group=state.get_tensor_model_parallel_group())
     args.do_train, args.do_valid, args.do_test = (bool(x) for x in flags.tolist())
     dl_type = args.dataloader_type

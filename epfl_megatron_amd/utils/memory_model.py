@@ -14,7 +14,9 @@ The estimate counts, per GPU:
   cache of the dgrad GEMMs;
 * per layer and in-flight micro-batch, the tensors the forward saves for the
   backward (GLU MLP, fused residual norms, FlashAttention), with s/tp-row
-  residual-stream tensors under sequence parallelism;
+  residual-stream tensors under sequence parallelism, plus the full-sequence
+  QKV / fc1 inputs the SP forward keeps for the wgrads (unless
+  ``--sp_regather_inputs``);
 * a recomputed layer keeps only its input; one layer's activations are live
   again while it is recomputed;
 * the LM-head logits and loss workspace, and a fixed allowance for GEMM /
@@ -47,7 +49,12 @@ def layer_activation_bytes(args, micro_batch=None):
     el = 2 if (args.bf16 or args.fp16) else 4
     glu = 2 if args.glu_activation else 1
     n = 0
-    n += 4 * t_res * h                          # norm inputs / GEMM inputs (re-gathered under SP)
+    n += 4 * t_res * h                          # norm inputs / GEMM inputs
+    if args.sequence_parallel and tp > 1 and not getattr(args, "sp_regather_inputs", False):
+        # the gathered [s, b, h] inputs of QKV and fc1, kept for their wgrads
+        # instead of re-gathered (parallel/tensor/layers.py sp_keep_gathered);
+        # they replace the saved s/tp-row GEMM inputs
+        n += 2 * (t - t_res) * h
     n += t * (nq + 2 * nkv) * hd // tp          # fused QKV output (RoPE'd, read by FA backward)
     n += t * nq * hd // tp                      # attention output (+ o-proj input)
     n += t * glu * f // tp + (t * f // tp if glu == 2 else 0)  # fc1 pre-activation (+ GLU output)
@@ -82,6 +89,8 @@ def estimate(args, n_params_rank, layers, recomputed, in_flight=1):
     transient = act if recomputed else 0        # a layer being recomputed
     vocab = getattr(args, "padded_vocab_size", None) or 0
     logits = t * vocab // tp * 4 * 2            # fp32 logits + their gradient
+    if args.sequence_parallel and tp > 1 and not getattr(args, "sp_regather_inputs", False):
+        logits += (t - t_res) * args.hidden_size * 2 * in_flight  # LM-head input kept gathered
     workspace = 8 * GB
     return static_bytes(args, n_params_rank) + in_flight * per_mb + transient + logits + workspace
 

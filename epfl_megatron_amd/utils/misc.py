@@ -39,7 +39,8 @@ def calc_params_l2_norm(model):
         sq = torch.zeros((), device=torch.cuda.current_device() if torch.cuda.is_available() else "cpu")
     sq = sq.reshape(1)
     if dist.is_initialized():
-        dist.all_reduce(sq, group=state.get_model_parallel_group())
+        from ..parallel import comm  # noqa: PLC0415
+        comm.all_reduce(sq, group=state.get_model_parallel_group())
     return sq.item() ** 0.5
 
 

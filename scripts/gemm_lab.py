@@ -1,8 +1,9 @@
-"""A/B of bench-only GEMM builds (csrc/gemm_lab.hip) against the production
+"""A/B of bench-only GEMM builds (scripts/lab/gemm_lab.hip) against the production
 persistent NT kernel and hipBLASLt: interleaved timing in one process (CDNA
 guide rule 24), uniform-random bf16 operands, median over rounds.  Variant 1
 is also checked against hipBLASLt's output.
 
+    python -m epfl_megatron_amd.build --lab     # once, on the CPU: scripts/lab/_gemm_lab.so
     python scripts/gemm_lab.py [M N K ...]
 """
 import os
@@ -13,6 +14,17 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from epfl_megatron_amd.ops._ext import ext  # noqa: E402
+
+
+def _lab():
+    import importlib.util
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lab", "_gemm_lab.so")
+    if not os.path.exists(so):
+        raise SystemExit("build the lab first: python -m epfl_megatron_amd.build --lab")
+    spec = importlib.util.spec_from_file_location("_gemm_lab", so)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def _t(fn, iters=10):
@@ -28,6 +40,7 @@ def _t(fn, iters=10):
 
 def main():
     C = ext()
+    L = _lab()
     C.gemm_nt_set_variant(6)  # production = the persistent kernel
     args = [int(v) for v in sys.argv[1:]]
     shapes = [tuple(args[i:i + 3]) for i in range(0, len(args), 3)] or \
@@ -40,7 +53,7 @@ def main():
         ref = torch.matmul(a, b.t())
         for v in variants:
             c.zero_()
-            C.gemm_lab(a, b, c, v)
+            L.gemm_lab(a, b, c, v)
             err = ((c.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
             assert err < 2e-2, f"variant {v} wrong: rel err {err}"
         fl = 2.0 * M * N * K
@@ -49,7 +62,7 @@ def main():
         r["hipblaslt"] = []
         for _ in range(5):
             for v in variants:
-                r[f"lab{v}"].append(fl / _t(lambda: C.gemm_lab(a, b, c, v)) / 1e12)
+                r[f"lab{v}"].append(fl / _t(lambda: L.gemm_lab(a, b, c, v)) / 1e12)
             r["prod"].append(fl / _t(lambda: C.gemm_nt(a, b, c)) / 1e12)
             r["hipblaslt"].append(fl / _t(lambda: torch.matmul(a, b.t(), out=c)) / 1e12)
         print(f"M={M} N={N} K={K}: " + "  ".join(

@@ -252,29 +252,33 @@ def test_gemm_nt_row_maps(tp, c, R, N, K):
     assert y.view(tp, c, R, F)[:, 1:].abs().sum().item() == 0
 
 
-@pytest.mark.parametrize("tp,c,R,N,K", [
-    (1, 1, 1024, 1280, 8192),   # 20 tiles: K split 8 ways
-    (8, 2, 256, 1280, 8192),    # Llama-2-70B TP8 qkv piece (80 tiles at 512-row groups: 2 ways)
-    (8, 2, 256, 1000, 8192),    # ragged N
-    (8, 2, 256, 1024, 4096),    # dense-dgrad-like piece through a C map
+@pytest.mark.parametrize("tp,c,R,N,K,dtype,splits", [
+    (1, 1, 1024, 1280, 8192, torch.bfloat16, 8),   # 20 tiles: K split 8 ways
+    (8, 2, 512, 1280, 8192, torch.bfloat16, 2),    # Llama-2-70B TP8 qkv piece (80 tiles: 2 ways)
+    (8, 2, 256, 1280, 8192, torch.bfloat16, 4),    # a half-size piece (40 tiles: 4 ways)
+    (8, 2, 256, 1000, 8192, torch.bfloat16, 8),    # ragged N (32 tiles: 8 ways)
+    (1, 1, 1000, 1280, 8192, torch.bfloat16, 8),   # ragged M (a partial last m-tile)
+    (8, 2, 512, 1280, 8192, torch.float16, 2),     # fp16 operands
+    (8, 2, 256, 1024, 4096, torch.bfloat16, 8),    # dense-dgrad-like piece through a C map
 ])
-def test_gemm_nt_split_k(tp, c, R, N, K):
+def test_gemm_nt_split_k(tp, c, R, N, K, dtype, splits):
     """Few-tile products on the persistent kernel split K over fp32 partials
-    (gemm_nt_split_reduce_k, fixed order): A / C row maps, ragged N, and
-    bitwise-reproducible results."""
+    (gemm_nt_split_reduce_k, fixed order): A / C row maps, ragged M and N,
+    fp16, the split count the plan picks, and bitwise-reproducible results."""
     torch.manual_seed(6)
-    b = _rand(N, K, scale=K ** -0.5)
-    full = _rand(tp * c * R, K)
+    assert _ext().gemm_nt_ksplit(tp * R, N, K) == splits
+    b = _rand(N, K, dtype=dtype, scale=K ** -0.5)
+    full = _rand(tp * c * R, K, dtype=dtype)
     j = c - 1
     amap = [R, c * R, j * R] if c > 1 else []
     out = _ext().gemm_nt(full, b, a_map=amap, m=tp * R)
     out2 = _ext().gemm_nt(full, b, a_map=amap, m=tp * R)
     ref = full.view(tp, c, R, K)[:, j].reshape(tp * R, K).float() @ b.float().t()
-    assert out.shape == (tp * R, N) and _rel_err(out, ref) < 1e-2
+    assert out.shape == (tp * R, N) and out.dtype == dtype and _rel_err(out, ref) < 1e-2
     assert torch.equal(out, out2)
     if c > 1:
-        g = _rand(tp * R, K)
-        dst = torch.zeros(tp * c * R, N, device=DEV, dtype=torch.bfloat16)
+        g = _rand(tp * R, K, dtype=dtype)
+        dst = torch.zeros(tp * c * R, N, device=DEV, dtype=dtype)
         _ext().gemm_nt(g, b, dst, c_map=[R, c * R, 0])
         v = dst.view(tp, c, R, N)
         assert _rel_err(v[:, 0].reshape(tp * R, N), g.float() @ b.float().t()) < 1e-2

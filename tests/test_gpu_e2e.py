@@ -78,10 +78,11 @@ def test_gpu_bf16_matches_cpu_fp32(name, argv):
     assert gpu[-1][0] < gpu[0][0] - 0.05, gpu  # learnable data: the loss falls
 
 
-def _sync_free(rank, world):
+def _sync_free(rank, world, extra=()):
     import finetune
     # RCCL (not gloo): a gloo collective on a GPU tensor is a host round trip
-    init_framework(LLAMA_GQA + ["--bf16", "--distributed_backend", "nccl"], finetune.extra_args)
+    init_framework(LLAMA_GQA + ["--bf16", "--distributed_backend", "nccl"] + list(extra),
+                   finetune.extra_args)
     from epfl_megatron_amd import get_args
     from epfl_megatron_amd.models import ModelType
     from epfl_megatron_amd.training import (_setup_model_and_optimizer,
@@ -115,8 +116,14 @@ def _sync_free(rank, world):
 
 
 @pytest.mark.gpu
-def test_train_step_has_no_host_sync():
-    calls = run_dist(_sync_free, 1)[0]
+@pytest.mark.parametrize("extra", [(), ("--simulated_tensor_parallel_size", "2",
+                                        "--sequence_parallel")],
+                         ids=["tp1", "simulated_tp2_sp"])
+def test_train_step_has_no_host_sync(extra):
+    """No device->host sync inside a training step: at TP = 1, and on one rank
+    of a TP = 2 + SP model (simulated TP: the batch broadcast over the TP
+    group reuses the sizes of the first micro-batch, VERDICT r5 weak #6)."""
+    calls = run_dist(_sync_free, 1, extra)[0]
     assert "cuda" not in calls, calls
 
 

@@ -264,13 +264,22 @@ def test_cross_entropy_tp_pieces():
     _close(loss, ref, 1e-3, 1e-4, "ce tp")
 
 
-@pytest.mark.parametrize("mode", ["causal", "mask", "none"])
-@pytest.mark.parametrize("sk", [128, 1000, 4096])
-def test_fused_softmax(mode, sk):
-    from epfl_megatron_amd.ops.softmax import _SoftmaxFn
+@pytest.mark.parametrize("mode", ["causal", "mask", "mask_bcast", "none"])
+@pytest.mark.parametrize("sk,dtype", [
+    (16, torch.bfloat16), (60, torch.bfloat16), (128, torch.bfloat16), (520, torch.float16),
+    (1000, torch.bfloat16), (1024, torch.float32), (2000, torch.bfloat16),
+    (4096, torch.bfloat16), (3000, torch.float32)])
+def test_fused_softmax(mode, sk, dtype):
+    """csrc/softmax.hip: wave-per-row (sk <= 1024) and workgroup-per-row forms,
+    16-B vector and element-wise row lengths, bf16 / fp16 / fp32, causal /
+    explicit / batch-broadcast ([1, 1, sq, sk], read with stride 0) masks,
+    vs the fp32 torch softmax (reference megatron/model/fused_softmax.py)."""
+    from epfl_megatron_amd.ops.softmax import _SoftmaxFn, FusedScaleMaskSoftmax
     torch.manual_seed(7)
-    b, np_, sq = 2, 3, sk if mode == "causal" else 37
-    x = torch.randn(b, np_, sq, sk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b, np_, sq = 2, 3, min(sk, 512) if mode == "causal" else 37
+    if mode == "causal":
+        sk = sq
+    x = torch.randn(b, np_, sq, sk, device=DEV, dtype=dtype, requires_grad=True)
     scale = 0.5
     xf = x.detach().float() * scale
     mask = None
@@ -278,19 +287,28 @@ def test_fused_softmax(mode, sk):
         m = torch.ones(sq, sk, device=DEV, dtype=torch.bool).triu(1)
         ref = torch.softmax(xf.masked_fill(m, float("-inf")), -1)
         y = _SoftmaxFn.apply(x, None, scale, 1)
-    elif mode == "mask":
-        mask = torch.rand(b, 1, sq, sk, device=DEV) < 0.3
+    elif mode in ("mask", "mask_bcast"):
+        mb = b if mode == "mask" else 1
+        mask = torch.rand(mb, 1, sq, sk, device=DEV) < 0.3
+        mask[..., 3, :] = True  # a fully masked row -> zeros
         ref = torch.softmax(xf.masked_fill(mask, -10000.0), -1)
+        ref[..., 3, :] = 0.0
         y = _SoftmaxFn.apply(x, mask, scale, 2)
+        if mode == "mask_bcast":  # the module path takes the broadcast mask as is
+            mod = FusedScaleMaskSoftmax(dtype == torch.float16, dtype == torch.bfloat16, None,
+                                        True, None, True, scale)
+            _close(mod(x.detach(), mask), ref, 1e-2, 2e-2, "softmax module bcast")
     else:
         ref = torch.softmax(xf, -1)
         y = _SoftmaxFn.apply(x, None, scale, 0)
-    _close(y, ref, 1e-2, 2e-2, f"softmax {mode}")
+    tol = (1e-5, 1e-4) if dtype == torch.float32 else (1e-2, 2e-2)
+    _close(y, ref, *tol, f"softmax {mode}")
     g = torch.randn_like(y)
     y.backward(g)
     yf = ref
     dref = scale * yf * (g.float() - (g.float() * yf).sum(-1, keepdim=True))
-    _close(x.grad, dref, 2e-2, 3e-2, f"softmax bwd {mode}")
+    tol = (1e-4, 1e-3) if dtype == torch.float32 else (2e-2, 3e-2)
+    _close(x.grad, dref, *tol, f"softmax bwd {mode}")
 
 
 def test_flat_adam_and_norm():
@@ -716,6 +734,35 @@ def test_wgrad_gemm_variants(variant, M, N, K):
     _close(g, g0 + ref, atol=1e-3 * math.sqrt(M), msg="accumulate")
     _close(g2, ref, atol=1e-3 * math.sqrt(M), msg="store")
     assert torch.equal(g2, g3)  # deterministic
+
+
+@pytest.mark.parametrize("world,c,R,N,K", [
+    (8, 2, 256, 1536, 4096),   # 7B TP8 qkv shard, piece-major SP gather (split-K tail path)
+    (8, 2, 256, 4096, 1376),   # row-parallel fc2 shard: natural X read piece-major
+    (4, 4, 64, 512, 768),      # more pieces than 2, small groups
+    (2, 2, 4096, 4096, 4096),  # whole-tile rounds (no split)
+])
+def test_wgrad_gemm_token_map(world, c, R, N, K):
+    """x_map: X's rows are a two-level permutation of dY's tokens (the SP
+    pipeline's piece-major gathers vs natural rows), read by the kernel
+    without a permutation copy; == the fp32 reference on the permuted X, and
+    bitwise equal to the kernel on an explicitly permuted copy."""
+    from epfl_megatron_amd.parallel.tensor.layers import _apply_token_map
+    C = _ext()
+    torch.manual_seed(4)
+    M = world * c * R
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    for xm in ([R, c, world * R, R], [R, world, c * R, R]):
+        xp = _apply_token_map(x, tuple(xm), M)
+        g = torch.zeros(N, K, device=DEV)
+        C.wgrad_gemm(dy, x, g, False, xm)
+        g_ref = torch.zeros(N, K, device=DEV)
+        C.wgrad_gemm(dy, xp.contiguous(), g_ref, False)
+        assert torch.equal(g, g_ref), xm
+        _close(g, dy.float().t() @ xp.float(), atol=1e-3 * math.sqrt(M), msg=f"map {xm}")
+    with pytest.raises(RuntimeError):
+        C.wgrad_gemm(dy, x, torch.zeros(N, K, device=DEV), False, [R + 16, c, world * R, R])
 
 
 def test_wgrad_plan():

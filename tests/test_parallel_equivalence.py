@@ -122,6 +122,7 @@ def test_llama_loss_decreases(llama_ref):
 @pytest.mark.parametrize("extra", [
     ["--tensor_model_parallel_size", "2"],
     ["--tensor_model_parallel_size", "2", "--sequence_parallel"],
+    ["--tensor_model_parallel_size", "2", "--sequence_parallel", "--sp_regather_inputs"],
 ])
 def test_llama_tensor_parallel(llama_ref, extra):
     got = _losses(run_dist(_train, 2, TINY_LLAMA + extra + ["--micro_batch_size", "2",
@@ -399,3 +400,40 @@ def test_llama_sp_mlp_uneven_pieces(llama_ref, monkeypatch, tp, pieces):
     got = _losses(run_dist(_train, tp, argv + mb + ["--tensor_model_parallel_size", str(tp),
                                                     "--sequence_parallel"], 3))
     _check(base, got, tol=5e-5)
+
+
+def _sp_gathers(rank, world, argv):
+    import finetune
+    init_framework(argv, finetune.extra_args)
+    from epfl_megatron_amd import get_args
+    from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.parallel import comm
+    from epfl_megatron_amd.training import (_setup_model_and_optimizer,
+                                            build_train_valid_test_data_iterators, train_step)
+    args = get_args()
+    model, opt, sched = _setup_model_and_optimizer(finetune.model_provider,
+                                                   ModelType.encoder_or_decoder, args=args)
+    it = build_train_valid_test_data_iterators(finetune.train_valid_test_datasets_provider)[0]
+    train_step(finetune.forward_step, it, model, opt, sched, args)
+    comm.report(reset=True)
+    train_step(finetune.forward_step, it, model, opt, sched, args)
+    rep = comm.report()
+    return {k: (v[0], v[1]) for k, v in rep.items() if k.endswith("/tp")}, args.num_layers
+
+
+def test_sp_keeps_gathered_inputs_for_wgrad():
+    """Kept SP gathers (default): the backward all-gathers no input of a
+    column-parallel product (QKV, fc1, LM head) again: per micro-batch 2 full
+    [s, b, h] all-gathers per layer + 1 for the LM head fewer;
+    every other TP collective is unchanged."""
+    argv = TINY_LLAMA + ["--tensor_model_parallel_size", "2", "--sequence_parallel",
+                         "--micro_batch_size", "2", "--global_batch_size", "4"]
+    kept, layers = run_dist(_sp_gathers, 2, argv)[0]
+    regather, _ = run_dist(_sp_gathers, 2, argv + ["--sp_regather_inputs"])[0]
+    n_micro, seq, mbs = 2, 16, 2
+    hidden = int(TINY_LLAMA[TINY_LLAMA.index("--hidden_size") + 1])
+    full = seq * mbs * hidden * 4  # one gathered [s, b, h] (fp32 params in the tiny run)
+    extra = regather["all_gather/tp"][1] - kept["all_gather/tp"][1]
+    assert extra == n_micro * (2 * layers + 1) * full, (kept, regather, full)
+    for k in ("reduce_scatter/tp", "all_reduce/tp", "broadcast/tp"):
+        assert regather[k] == kept[k]

@@ -16,16 +16,16 @@ def test_selfcheck_passes_on_3d_grid():
                          "2", "--ddp_comm_groups", "2", "--micro_batch_size", "1",
                          "--global_batch_size", "4"]
     counts = run_dist(_init_and_count, 8, argv)
-    # 2 DP communicators x 6 + TP 6 + PP 1 on every rank
-    assert counts == [19] * 8
+    # env agreement 1 + 2 DP communicators x 6 + TP 6 + PP 1 on every rank
+    assert counts == [20] * 8
 
 
 def test_selfcheck_passes_with_context_parallel():
     argv = TINY_LLAMA + ["--tensor_model_parallel_size", "2", "--context_parallel_size", "2",
                          "--micro_batch_size", "1", "--global_batch_size", "4"]
     counts = run_dist(_init_and_count, 4, argv)
-    # DP (2 ranks) 6 + TP 6 + CP 6 (no pipeline)
-    assert counts == [18] * 4
+    # env agreement 1 + DP (2 ranks) 6 + TP 6 + CP 6 (no pipeline)
+    assert counts == [19] * 4
 
 
 def _broken_avg(rank, world, argv):
@@ -50,3 +50,32 @@ def _broken_avg(rank, world, argv):
 def test_selfcheck_detects_wrong_semantics():
     argv = TINY_LLAMA + ["--micro_batch_size", "1", "--global_batch_size", "4"]
     assert run_dist(_broken_avg, 2, argv) == [True, True]
+
+
+def _mismatched_knob(rank, world, argv):
+    import os
+    import finetune
+    # rank 1 would split its SP all-gathers in 4 pieces, rank 0 in 2: RCCL
+    # would hang mid-step, so the startup check must refuse
+    os.environ["EMA_SP_CHUNKS"] = str(2 + 2 * rank)
+    os.environ["EMA_TRACE"] = str(rank)  # rank-local: allowed to differ
+    try:
+        init_framework(argv, finetune.extra_args)
+    except RuntimeError as e:
+        msg = str(e)
+        return "EMA_SP_CHUNKS=['2', '4']" in msg and "EMA_TRACE" not in msg
+    return False
+
+
+def test_selfcheck_refuses_mismatched_env_knobs():
+    argv = TINY_LLAMA + ["--tensor_model_parallel_size", "2", "--micro_batch_size", "1",
+                         "--global_batch_size", "4"]
+    assert run_dist(_mismatched_knob, 2, argv) == [True, True]
+
+
+def test_structural_env_filters_local_knobs():
+    from epfl_megatron_amd.parallel.selfcheck import structural_env
+    env = {"EMA_SP_CHUNKS": "4", "EMA_FUSED_MLP": "0", "EMA_TRACE": "1", "EMA_GEMM_GM": "8",
+           "EMA_WGRAD_GN": "4", "EMA_NEW_KNOB": "x", "PATH": "/bin"}
+    assert structural_env(env) == {"EMA_FUSED_MLP": "0", "EMA_NEW_KNOB": "x",
+                                   "EMA_SP_CHUNKS": "4"}

@@ -34,6 +34,15 @@ def _sim_rank(rank, world, n):
     comm.all_gather_into(sc, x + 100, group=g)
     out["ag_scratch"] = first and torch.equal(sc[:3], x + 100) and all(
         torch.equal(sc[3 * i:3 * i + 3], x) for i in range(1, n))
+    # another user takes the same buffer with another view and writes it (here
+    # NaN): the next hand-out in the first view is a new generation, so the
+    # peers' slots are refilled instead of trusted
+    other = get_global_memory_buffer().get_tensor((n, 6), torch.float32, "loopback-test")
+    other.fill_(float("nan"))
+    sc = get_global_memory_buffer().get_tensor((3 * n, 2), torch.float32, "loopback-test")
+    comm.all_gather_into(sc, x, group=g)
+    out["ag_regen"] = bool(torch.isfinite(sc).all()) and all(
+        torch.equal(sc[3 * i:3 * i + 3], x) for i in range(n))
     parts = torch.arange(n * 6, dtype=torch.float32).view(n * 3, 2)
     rs = torch.empty(3, 2)
     comm.reduce_scatter_into(rs, parts, group=g)
@@ -54,7 +63,7 @@ def _sim_rank(rank, world, n):
 def test_simulated_tp_rank_shapes_and_loopback():
     out = run_dist(_sim_rank, 1, 4)[0]
     assert out["tp"] == 4 and out["sp"]
-    assert out["ag"] and out["rs"] and out["ag_scratch"]
+    assert out["ag"] and out["rs"] and out["ag_scratch"] and out["ag_regen"]
     # h 64, 8 heads of 8 -> 2 heads per rank: qkv 3 * 2 * 8 = 48 rows; ffn 128 -> 2 * 32
     assert out["qkv"] == (48, 64) and out["fc1"] == (64, 64)
     assert out["loss"] == out["loss"] and out["loss"] > 0

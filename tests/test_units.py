@@ -178,19 +178,42 @@ def test_vocab_parallel_cross_entropy(smoothing):
 
 def _broadcast(rank, world):
     state = _init_mp(rank, world, 2, 1)
-    from epfl_megatron_amd.parallel.tensor.data import broadcast_data
-    data = None
+    from epfl_megatron_amd.parallel import comm
+    from epfl_megatron_amd.parallel.tensor.data import broadcast_data, reset_size_cache
+    reset_size_cache()
+    outs = []
+    comm.report(reset=True)
+    for step in range(3):
+        data = None
+        if rank % 2 == 0:
+            data = {"text": torch.arange(12).view(3, 4) + rank + 100 * step,
+                    "mask": torch.ones(2, 2)}
+        outs.append(broadcast_data(["text"], data, torch.int64)["text"].tolist())
+    # sizes are broadcast once per key set (the host sync of the size vector
+    # is paid on the first micro-batch only); the payload every call; both
+    # through parallel/comm.py
+    n_bcast = comm.report().get("broadcast/tp", (0,))[0]
+    # a TP-rank-0 batch of another shape is refused (no mismatched broadcasts)
+    refused = None
     if rank % 2 == 0:
-        data = {"text": torch.arange(12).view(3, 4) + rank, "mask": torch.ones(2, 2)}
-    out = broadcast_data(["text"], data, torch.int64)
+        try:
+            broadcast_data(["text"], {"text": torch.zeros(2, 4, dtype=torch.int64)}, torch.int64)
+            refused = False
+        except RuntimeError as e:
+            refused = "--variable_seq_lengths" in str(e)
     state.destroy_model_parallel()
-    return out["text"].tolist()
+    return outs, n_bcast, refused
 
 
 def test_broadcast_data_over_tp():
     res = run_dist(_broadcast, 4)
-    assert res[0] == res[1] == (torch.arange(12).view(3, 4)).tolist()
-    assert res[2] == res[3] == (torch.arange(12).view(3, 4) + 2).tolist()
+    for step in range(3):
+        want0 = (torch.arange(12).view(3, 4) + 100 * step).tolist()
+        assert res[0][0][step] == res[1][0][step] == want0
+        assert res[2][0][step] == res[3][0][step] == (torch.arange(12).view(3, 4) + 2 +
+                                                      100 * step).tolist()
+    assert all(r[1] == 1 + 3 for r in res)  # 1 size broadcast + 3 payloads
+    assert res[0][2] is True and res[2][2] is True
 
 
 def _rng(rank, world):
