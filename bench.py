@@ -423,6 +423,10 @@ def main(argv=None):
                 m.wait_param_sync()
         sync()
         diag = _comm_diag(comm.report(reset=True), (time.perf_counter() - t1) * 1e3)
+        fargs = get_args()
+        diag["model"] = {"layers_per_stage": fargs.num_layers // fargs.pipeline_model_parallel_size,
+                         "hidden": fargs.hidden_size,
+                         "bytes_per_el": 2 if (fargs.bf16 or fargs.fp16) else 4}
         comm.set_timing(False)
     optimizer.resolve_pending()
     tokens = par["gbs"] * par["seq"] * a.steps

@@ -49,7 +49,9 @@ FLAG_TABLE = {
         _flag("--max_tokens_to_oom", type=int, default=12000),
         _flag("--inference_hip_graph", action="store_true",
               help="replay single-token decode forwards from a captured hipGraph "
-                   "(TP = PP = 1; inference/hip_graph.py)"),
+                   "(any TP / PP size: under PP every stage replays its own graph between an "
+                   "eager receive and send; the whole-loop greedy decoder needs PP = 1; "
+                   "inference/hip_graph.py)"),
     ],
     "network size": [
         _flag("--num_layers", type=int, default=None),

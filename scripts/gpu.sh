@@ -13,6 +13,7 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py --steps 8 --warmup 2 (the headline config)
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --steps 2 --warmup 1
+#   prof4k / bench4k  the same profile / bench at seq 4096, micro-batch 4
 #   profpx7    rocprofv3 kernel trace of the llama7b-tp8 proxy (profpx70: llama70b-tp8)
 #   ab         bench.py twice plain / twice with $AB_ENV, interleaved
 #   scriptab   python $SCRIPT plain / with $AB_ENV, interleaved twice
@@ -71,6 +72,8 @@ for step in "$@"; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 500 python -u bench.py --steps 8 --warmup 2 $BENCH_ARGS ;;
     prof) prof prof 600 python3 -u bench.py --steps 2 --warmup 1 $BENCH_ARGS ;;
+    prof4k) prof prof4k 600 python3 -u bench.py --seq_len 4096 --micro_batch 4 --steps 2 --warmup 1 ;;
+    bench4k) run bench4k 500 python -u bench.py --seq_len 4096 --micro_batch 4 --steps 6 --warmup 2 ;;
     profpx7) prof profpx7 600 python3 -u bench.py --proxy llama7b-tp8 --steps 2 --warmup 1 ;;
     profpx70) prof profpx70 900 python3 -u bench.py --proxy llama70b-tp8 --steps 1 --warmup 1 ;;
     ab)  # interleaved bench A/B: plain, then with $AB_ENV (e.g. AB_ENV="EMA_X=1"), twice

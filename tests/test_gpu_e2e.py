@@ -85,8 +85,10 @@ def _sync_free(rank, world, extra=()):
                    finetune.extra_args)
     from epfl_megatron_amd import get_args
     from epfl_megatron_amd.models import ModelType
+    from epfl_megatron_amd.parallel import comm
     from epfl_megatron_amd.training import (_setup_model_and_optimizer,
                                             build_train_valid_test_data_iterators, train_step)
+    comm.set_race_check(False)  # (the debug checker compares buffers on the host)
     args = get_args()
     model, opt, sched = _setup_model_and_optimizer(finetune.model_provider,
                                                    ModelType.encoder_or_decoder, args=args)
@@ -122,8 +124,10 @@ def _sync_free(rank, world, extra=()):
 def test_train_step_has_no_host_sync(extra):
     """No device->host sync inside a training step: at TP = 1, and on one rank
     of a TP = 2 + SP model (simulated TP: the batch broadcast over the TP
-    group reuses the sizes of the first micro-batch, VERDICT r5 weak #6)."""
-    calls = run_dist(_sync_free, 1, extra)[0]
+    group reuses the sizes of the first micro-batch).
+    The debug race checker (conftest turns it on) compares buffers on the host
+    by design, so it is off here."""
+    calls = run_dist(_sync_free, 1, extra, env={"EMA_COMM_CHECK": "0"})[0]
     assert "cuda" not in calls, calls
 
 

@@ -201,9 +201,13 @@ def _rank_dead_peer(rank, world):
 
     from epfl_megatron_amd.parallel.xgmi import XgmiAllReduce, XgmiError
 
+    from epfl_megatron_amd.parallel import comm
+
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    xg = XgmiAllReduce(None, cap_bytes=64 * 1024)
+    # a short per-communicator bound (what a decode server may choose); the
+    # default is long (test_xgmi_slow_peer_is_not_a_timeout)
+    xg = XgmiAllReduce(None, cap_bytes=64 * 1024, timeout_ms=300)
     res = None
     if rank == 0:
         t = torch.ones(8192, dtype=torch.bfloat16, device="cuda")
@@ -211,15 +215,49 @@ def _rank_dead_peer(rank, world):
         xg(t)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        # the device error word folds into the grad-norm square: the step is
+        # skipped on device (comm.fold_xgmi_error), no host sync needed
+        comm._XGMI[id(None)] = xg
+        try:
+            folded = comm.fold_xgmi_error(torch.tensor([4.0], device="cuda")).item()
+        finally:
+            comm._XGMI.pop(id(None), None)
         try:
             xg.check()
             raised = False
         except XgmiError:
             raised = True
-        res = (bool(torch.isnan(t.float()).all().item()), raised, dt)
+        res = (bool(torch.isnan(t.float()).all().item()), raised, dt, folded, xg.timeout_ms)
     dist.barrier()
     xg.close()
     return res
+
+
+def _rank_slow_peer(rank, world):
+    """Rank 1 arrives 2.5 s late (host work: a checkpoint write, a GC pause):
+    with the default bound the call completes correctly on both ranks and
+    nothing is flagged."""
+    import time
+
+    import torch.distributed as dist
+
+    from epfl_megatron_amd.parallel.xgmi import XgmiAllReduce
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    xg = XgmiAllReduce(None, cap_bytes=64 * 1024)
+    dist.barrier()
+    if rank == 1:
+        time.sleep(2.5)
+    t = torch.full((8192,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
+    xg(t)
+    torch.cuda.synchronize()
+    ok = bool((t.float() == 3.0).all().item())
+    err = int(xg.error_tensor().item())
+    xg.check()
+    dist.barrier()
+    xg.close()
+    return ok, err, xg.timeout_ms
 
 
 def test_xgmi_sp_piece_allgather():
@@ -228,10 +266,16 @@ def test_xgmi_sp_piece_allgather():
 
 
 def test_xgmi_dead_peer_times_out():
-    res = run_dist(_rank_dead_peer, 2, timeout=300, env={"EMA_XGMI_TIMEOUT_MS": "300"})
-    all_nan, raised, dt = res[0]
-    assert all_nan and raised
+    res = run_dist(_rank_dead_peer, 2, timeout=300)
+    all_nan, raised, dt, folded, tmo = res[0]
+    assert all_nan and raised and tmo == 300
+    assert folded == float("inf")  # the optimizer skips the step
     assert dt < 5.0, dt  # bounded by the 300 ms wall-clock wait, not tens of seconds
+
+
+def test_xgmi_slow_peer_is_not_a_timeout():
+    for ok, err, tmo in run_dist(_rank_slow_peer, 2, timeout=300):
+        assert ok and err == 0 and tmo == 60000
 
 
 @pytest.mark.parametrize("world", [2, 4])
