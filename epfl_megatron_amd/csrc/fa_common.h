@@ -79,15 +79,6 @@ __device__ __forceinline__ void mfma_vgpr(f32x16& acc, typename MT<T>::x8 a,
     else asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
   }
 }
-// acc (AGPR) = 0 by an MFMA with C = 0 on zero operands (an accumulator that
-// only asm MFMAs ever touch stays in AGPRs from its definition on)
-template <typename T>
-__device__ __forceinline__ void mfma_agpr0_init(f32x16& acc, typename MT<T>::x8 z) {
-  if constexpr (__is_same(T, bf16))
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
-  else
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %1, 0" : "=a"(acc) : "v"(z));
-}
 // acc = A * B (C = 0), VGPR destination
 template <typename T>
 __device__ __forceinline__ f32x16 mfma_vgpr0(typename MT<T>::x8 a, typename MT<T>::x8 b) {
@@ -138,23 +129,6 @@ __device__ __forceinline__ typename MT<T>::x4 tr_read_imm(uint32_t base) {
   static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
   typename MT<T>::x4 r;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF));
-  return r;
-}
-// ds_read_b128 with a folded immediate, as asm (same reason as tr_read_imm).
-template <int OFF, typename T>
-__device__ __forceinline__ typename MT<T>::x8 row_read_imm(uint32_t base) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
-  typename MT<T>::x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF));
-  return r;
-}
-// ds_read_b128 straight into AGPRs (an MFMA operand that VALU never touches:
-// it frees 4 arch VGPRs per fragment at one wave per SIMD).
-template <int OFF, typename T>
-__device__ __forceinline__ typename MT<T>::x8 row_read_imm_a(uint32_t base) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
-  typename MT<T>::x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=a"(r) : "v"(base), "i"(OFF));
   return r;
 }
 // Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N).

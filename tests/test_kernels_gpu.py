@@ -417,28 +417,6 @@ def test_flash_attention_fp16():
     _attn_case(1, 192, 4, 4, 128, torch.float16, True)
 
 
-@pytest.mark.parametrize("case", ["causal", "full", "odd", "gqa2k", "fp16", "maxjump", "docs"])
-def test_flash_attention_fwd_v2(case, monkeypatch):
-    """The opt-in 4-wave forward (EMA_FA_FWD=2: two pipelined 32-row
-    sub-blocks per wave, lazy rescale) on the shapes and branches of the
-    default kernel's tests."""
-    monkeypatch.setenv("EMA_FA_FWD", "2")
-    if case == "causal":
-        _attn_case(2, 256, 4, 4, 128, torch.bfloat16, True)
-    elif case == "full":
-        _attn_case(2, 320, 8, 2, 128, torch.bfloat16, False, seed=3)
-    elif case == "odd":
-        _attn_case(1, 1000, 4, 2, 128, torch.bfloat16, True, seed=5)
-    elif case == "gqa2k":
-        _attn_case(1, 2048, 16, 4, 128, torch.bfloat16, True, seed=7)
-    elif case == "fp16":
-        _attn_case(1, 192, 4, 4, 128, torch.float16, True)
-    elif case == "maxjump":
-        test_flash_attention_running_max_jump()
-    else:
-        test_flash_attention_document_mask(600, 2, 2, 3, 128)
-
-
 @pytest.mark.parametrize("s,b,ng,r,hd,with_pos", [
     (300, 2, 2, 3, 128, False),   # GQA, dK/dV split over query heads (reduce-kernel epilogue)
     (4096, 1, 2, 1, 128, False),  # Llama-2 native context, MHA (dK/dV kernel epilogue)
