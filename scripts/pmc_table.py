@@ -8,7 +8,8 @@ mean per dispatch, then derived ratios where the counters are present:
   wait%  = SQ_WAIT_ANY / SQ_WAVE_CYCLES, stall% = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES,
   active% = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES (these three partition wave time),
   mfma%  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs),
-  conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, L2hit = TCC_HIT / (HIT + MISS).
+  conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, L2hit = TCC_HIT / (HIT + MISS),
+  us     = mean dispatch duration (Start/End_Timestamp), GHz = GRBM_GUI_ACTIVE / 8 XCDs / us.
 """
 import csv
 import glob
@@ -19,15 +20,21 @@ from collections import defaultdict
 
 def main():
     vals = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)
     for d in sys.argv[1:]:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             per = defaultdict(float)  # (kernel, dispatch, counter) -> summed over dimensions
+            span = {}
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    per[(row["Kernel_Name"][:60], row.get("Dispatch_Id", "0"), row["Counter_Name"])] += \
-                        float(row["Counter_Value"])
+                    key = (row["Kernel_Name"][:60], row.get("Dispatch_Id", "0"))
+                    per[key + (row["Counter_Name"],)] += float(row["Counter_Value"])
+                    if row.get("Start_Timestamp") and row.get("End_Timestamp"):
+                        span[key] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
             for (k, _, c), v in per.items():
                 vals[k][c].append(v)
+            for (k, _), ns in span.items():
+                durs[k].append(ns)
     for k, cs in vals.items():
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
         n = max(len(v) for v in cs.values())
@@ -50,6 +57,11 @@ def main():
         if "TCC_HIT_sum" in mean:
             h, m = mean["TCC_HIT_sum"], mean.get("TCC_MISS_sum", 0)
             d.append(f"L2hit={100 * h / max(h + m, 1):.1f}%")
+        if durs.get(k):
+            us = sum(durs[k]) / len(durs[k]) / 1e3
+            d.append(f"us={us:.1f}")
+            if g:
+                d.append(f"GHz={g / 8 / (us * 1e3):.2f}")
         if d:
             print("   -> " + "  ".join(d))
 
