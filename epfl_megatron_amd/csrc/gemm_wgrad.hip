@@ -676,13 +676,16 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
   return pl.nsplit > 1 ? (int64_t)pl.nsplit * pl.tail_tiles * TN * TK : 0;
 }
 
-// Kernel for the whole-tile rounds: 8 = the 8-wave ping-pong wgrad_k
-// (default), 4 = the persistent 4-wave wgrad4_k (EMA_WGRAD_V=4 /
-// wgrad_set_variant: A/B; measured 0.83-0.95x of the 8-wave kernel on the 7B
-// shapes, profiles/r4a_wgrad_variants.txt).
+// Kernel for the whole-tile rounds: 4 = the persistent 4-wave wgrad4_k
+// (default since round 6), 8 = the 8-wave ping-pong wgrad_k (EMA_WGRAD_V=8 /
+// wgrad_set_variant: A/B).  Round 4 measured the 4-wave kernel at 0.83-0.95x
+// (profiles/r4a_wgrad_variants.txt); with the vendor slot plan it shares with
+// gemm_nt6_k since round 5 it is 1.02-1.07x isolated and +1.6 % on the
+// headline step (profiles/r7r_wgrad_v4_ab.txt).  Token-mapped X (kept SP
+// gathers), M % 64 != 0 and > 2 GiB operands stay on wgrad_k.
 int g_wvar = [] {
   const char* e = getenv("EMA_WGRAD_V");
-  return (e && e[0] == '4') ? 4 : 8;
+  return (e && e[0] == '8') ? 8 : 4;
 }();
 
 int num_cus() {
@@ -745,6 +748,6 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   }
 }
 
-void wgrad_set_variant(int v) { g_wvar = v == 4 ? 4 : 8; }
+void wgrad_set_variant(int v) { g_wvar = v == 8 ? 8 : 4; }
 
 }  // namespace ema
