@@ -583,15 +583,16 @@ int tile_group(int ntn, int ntk) {
   return ntn >= ntk ? -4 : 8;
 }
 
+// gn: the tile order, shared by every launch of one wgrad_gemm (the main
+// rounds and the split tail partition ONE order: both must use the same gn)
 template <typename T, bool ACCUM>
-void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s,
+void launch(const void* dy, const void* x, float* g, int M, int N, int K, hipStream_t s, int gn,
             int nsplit = 1, float* ws = nullptr, int lin0 = 0, int nlin = -1, TokMap xm = {}) {
   const int ntiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
   if (nlin < 0) nlin = ntiles;
   const int msplit = ((M / nsplit + BM - 1) / BM) * BM;
   hipLaunchKernelGGL((wgrad_k<T, ACCUM>), dim3(nlin * nsplit), dim3(512), 0, s,
-                     (const T*)dy, (const T*)x, g, M, N, K,
-                     tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), msplit,
+                     (const T*)dy, (const T*)x, g, M, N, K, gn, msplit,
                      nsplit > 1 ? ws : nullptr, lin0, nlin, xm);
 }
 
@@ -704,11 +705,24 @@ bool wgrad4_ok(int64_t M, int64_t N, int64_t K) {
   return g_wvar == 4 && M % 64 == 0 && M >= 128 && M * N * 2 < lim && M * K * 2 < lim;
 }
 
+// Tile grouping of the persistent kernel: groups of 8 n-tiles x all k-tiles on
+// every 7B shape (sweep on one box, profiles/r7t_wgrad4_group_sweep.txt: qkv
+// +3.2 %, fc1 +4.1 %, lm_head +2.6 % over the 8-wave kernel's rule, dense /
+// fc2 within noise); EMA_WGRAD_GN overrides both kernels.
+int tile_group4() {
+  static const int env = [] {
+    const char* e = getenv("EMA_WGRAD_GN");
+    return e ? atoi(e) : 0;
+  }();
+  return env != 0 ? env : 8;
+}
+
 template <typename T, bool ACCUM>
-void launch4(const void* dy, const void* x, float* g, int M, int N, int K, int tiles, hipStream_t s) {
+void launch4(const void* dy, const void* x, float* g, int M, int N, int K, int tiles, int gn,
+             hipStream_t s) {
   const int grid = tiles < num_cus() ? tiles : num_cus();
   hipLaunchKernelGGL((wgrad4_k<T, ACCUM>), dim3(grid), dim3(256), 0, s, (const T*)dy, (const T*)x, g,
-                     M, N, K, tile_group((N + TN - 1) / TN, (K + TK - 1) / TK), tiles);
+                     M, N, K, gn, tiles);
 }
 
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
@@ -718,32 +732,32 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   const bool split = pl.nsplit > 1 && ws != nullptr;
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
   if (xm.rows != 0 && xm.rows % BM != 0) throw std::runtime_error("wgrad: token map groups must be 32-row multiples");
-  if (main_tiles > 0 && xm.rows == 0 && wgrad4_ok(M, N, K)) {
+  const bool v4 = main_tiles > 0 && xm.rows == 0 && wgrad4_ok(M, N, K);
+  const int gn = v4 ? tile_group4() : tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK);
+  if (v4) {
     if (dt == DT_BF16) {
-      if (accumulate) launch4<bf16, true>(dy, x, g, iM, iN, iK, main_tiles, s);
-      else launch4<bf16, false>(dy, x, g, iM, iN, iK, main_tiles, s);
+      if (accumulate) launch4<bf16, true>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
+      else launch4<bf16, false>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
     } else if (dt == DT_F16) {
-      if (accumulate) launch4<fp16, true>(dy, x, g, iM, iN, iK, main_tiles, s);
-      else launch4<fp16, false>(dy, x, g, iM, iN, iK, main_tiles, s);
+      if (accumulate) launch4<fp16, true>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
+      else launch4<fp16, false>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
     }
-  } else
-  if (main_tiles > 0) {
+  } else if (main_tiles > 0) {
     if (dt == DT_BF16) {
-      if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
-      else launch<bf16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
+      if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, gn, 1, nullptr, 0, main_tiles, xm);
+      else launch<bf16, false>(dy, x, g, iM, iN, iK, s, gn, 1, nullptr, 0, main_tiles, xm);
     } else if (dt == DT_F16) {
-      if (accumulate) launch<fp16, true>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
-      else launch<fp16, false>(dy, x, g, iM, iN, iK, s, 1, nullptr, 0, main_tiles, xm);
+      if (accumulate) launch<fp16, true>(dy, x, g, iM, iN, iK, s, gn, 1, nullptr, 0, main_tiles, xm);
+      else launch<fp16, false>(dy, x, g, iM, iN, iK, s, gn, 1, nullptr, 0, main_tiles, xm);
     }
   }
   if (split) {
     if (dt == DT_BF16)
-      launch<bf16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
+      launch<bf16, false>(dy, x, g, iM, iN, iK, s, gn, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
     else if (dt == DT_F16)
-      launch<fp16, false>(dy, x, g, iM, iN, iK, s, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
+      launch<fp16, false>(dy, x, g, iM, iN, iK, s, gn, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
-                       ws, g, iN, iK, tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK),
-                       pl.tail_lin0, pl.tail_tiles,
+                       ws, g, iN, iK, gn, pl.tail_lin0, pl.tail_tiles,
                        pl.nsplit, accumulate ? 1 : 0);
   }
 }
