@@ -398,13 +398,36 @@ __device__ __forceinline__ void wmfma0(f32x4_& acc, typename fa::MT<T>::x8 a, ty
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
 
-template <typename T, bool ACCUM>
-__global__ void __launch_bounds__(256, 1)
-wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ g, int M, int N,
-         int K, int gn, int ntiles) {
+// Arguments of the persistent 4-wave kernel.  Items: whole tiles [0, nitems)
+// over all M tokens, or (SPLIT) token pieces of the tiles [lin0, lin0 + nlin):
+// item it = piece (it / nlin) of tile lin0 + it % nlin, msplit tokens each,
+// stored as an fp32 block ws[it] for wgrad_split_reduce_k (the 8-wave
+// kernel's split-major layout).  TM: X rows through the token map xm (xrows:
+// the physical X rows it reaches).
+struct W4Args {
+  const void* dy;
+  const void* x;
+  float* g;
+  float* ws;
+  int M, N, K, msplit, gn, nitems, lin0, nlin, xrows;
+  TokMap xm;
+};
+
+// 32-bit form of tok_row (the host bounds xrows * K * 2 below 2^31)
+__device__ __forceinline__ int tok_row32(int q, const TokMap& m) {
+  const int grp = (int)((unsigned)q / (unsigned)m.rows);
+  const int n1 = m.n1;
+  return (grp % n1) * (int)m.s1 + (grp / n1) * (int)m.s2 + (q - grp * m.rows);
+}
+
+template <typename T, bool ACCUM, bool TM, bool SPLIT>
+__global__ void __launch_bounds__(256, 1) wgrad4_k(W4Args a) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * SLOTB2];
   typedef typename fa::MT<T>::x8 X8;
   typedef typename fa::MT<T>::x4 X4;
+  const T* __restrict__ dy = (const T*)a.dy;
+  const T* __restrict__ x = (const T*)a.x;
+  const int M = a.M, N = a.N, K = a.K, gn = a.gn, ntiles = a.nitems;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave >> 1, wk = wave & 1;
@@ -412,7 +435,7 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
   if (bid >= ntiles) return;
   const int nmine = (ntiles - 1 - bid) / G + 1;
   const int ntn = (N + TN - 1) / TN, ntk = (K + TK - 1) / TK;
-  const int nt = M / 64;  // >= 2 (host-checked)
+  const int nt = (SPLIT ? a.msplit : M) / 64;  // >= 2 (host-checked)
 
   // per-lane DMA offset of a piece (rows 8 wave .. of an image, 512 B per row)
   auto lane_off = [&](int ld) {
@@ -424,36 +447,56 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
   const uint32_t srow_a = (uint32_t)(8 * wave * N * (int)sizeof(T));
   const uint32_t srow_b = (uint32_t)(8 * wave * K * (int)sizeof(T));
 
-  auto tile_org = [&](int i, int64_t& n0, int64_t& k0) {
+  // item i of this workgroup: output tile origin, first token, ws block
+  auto tile_org = [&](int i, int64_t& n0, int64_t& k0, int& t0, int& blk) {
     const int base = i * G, rem = min(G, ntiles - base);
-    const int2 tt = tile_of(base + xcd_remap(bid, rem), ntn, ntk, gn);
+    const int it = base + xcd_remap(bid, rem);
+    const int sp = SPLIT ? it / a.nlin : 0;
+    const int lin = SPLIT ? a.lin0 + (it - sp * a.nlin) : it;
+    const int2 tt = tile_of(lin, ntn, ntk, gn);
     n0 = (int64_t)tt.x * TN;
     k0 = (int64_t)tt.y * TK;
+    t0 = sp * a.msplit;
+    blk = it;
   };
-  auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb) {
-    int64_t n0 = 0, k0 = 0, na = 0, nb = 0;
+  // buffer descriptors of item i (q0: its first logical token, for TM)
+  auto make_rsrc = [&](int i, Rsrc& ra, Rsrc& rb, int& q0) {
+    int64_t n0 = 0, k0 = 0, na = 0, nb = 0, oa = 0, ob = 0;
+    int t0 = 0, blk = 0;
     if (i < nmine) {
-      tile_org(i, n0, k0);
-      na = ((int64_t)M * N - n0) * (int64_t)sizeof(T);
-      nb = ((int64_t)M * K - k0) * (int64_t)sizeof(T);
+      tile_org(i, n0, k0, t0, blk);
+      oa = (int64_t)t0 * N + n0;
+      ob = TM ? k0 : (int64_t)t0 * K + k0;
+      na = ((int64_t)M * N - oa) * (int64_t)sizeof(T);
+      nb = ((int64_t)(TM ? a.xrows : M) * K - ob) * (int64_t)sizeof(T);
     }
-    ra = __builtin_amdgcn_make_buffer_rsrc((void*)(dy + n0), 0, (int)na, 0x00020000);
-    rb = __builtin_amdgcn_make_buffer_rsrc((void*)(x + k0), 0, (int)nb, 0x00020000);
+    q0 = t0;
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)(dy + oa), 0, (int)na, 0x00020000);
+    rb = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ob), 0, (int)nb, 0x00020000);
   };
   char* const ldsp = lds;
   // piece i (0..3) of image kh of operand op, K-step s, into slot
-  auto dma = [&](int op, int kh, int i, Rsrc r, int s, int slot) {
+  // (xr: TM's byte offsets of the step's two physical X row blocks)
+  auto dma = [&](int op, int kh, int i, Rsrc r, int s, int slot, const uint32_t (&xr)[2]) {
     const int ld = op ? K : N;
-    const uint32_t soff = (uint32_t)((s * 64 + 32 * kh) * ld * (int)sizeof(T)) + (op ? srow_b : srow_a) +
-                          128u * (uint32_t)i;
+    const uint32_t rows = (TM && op) ? xr[kh] : (uint32_t)((s * 64 + 32 * kh) * ld * (int)sizeof(T));
+    const uint32_t soff = rows + (op ? srow_b : srow_a) + 128u * (uint32_t)i;
     const int dst = slot * SLOTB2 + op * OPB2 + kh * IMG + (4 * wave + i) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ldsp + dst),
                                              16, op ? voff_b : voff_a, soff, 0, 0);
   };
   // DMA piece q (0..7 dY, 8..15 X) of a K-step
-  auto dmaq = [&](int q, Rsrc ra, Rsrc rb, int s, int slot) {
+  auto dmaq = [&](int q, Rsrc ra, Rsrc rb, int s, int slot, const uint32_t (&xr)[2]) {
     const int op = q >> 3, kh = (q >> 2) & 1, i = q & 3;
-    dma(op, kh, i, op ? rb : ra, s, slot);
+    dma(op, kh, i, op ? rb : ra, s, slot, xr);
+  };
+  auto xrows_of = [&](int q0, int s, uint32_t (&xr)[2]) {
+    if constexpr (TM) {
+      xr[0] = (uint32_t)tok_row32(q0 + 64 * s, a.xm) * (uint32_t)(K * (int)sizeof(T));
+      xr[1] = (uint32_t)tok_row32(q0 + 64 * s + 32, a.xm) * (uint32_t)(K * (int)sizeof(T));
+    } else {
+      xr[0] = xr[1] = 0;
+    }
   };
 
   f32x4_ acc[8][8];
@@ -479,10 +522,16 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
   using K1 = std::integral_constant<int, 1>;
 
   Rsrc ra_c, rb_c, ra_n, rb_n;
-  make_rsrc(0, ra_c, rb_c);
-  make_rsrc(1, ra_n, rb_n);
-  static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 0, 0); });
-  static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 1, 1); });
+  int q_c, q_n;
+  make_rsrc(0, ra_c, rb_c, q_c);
+  make_rsrc(1, ra_n, rb_n, q_n);
+  {
+    uint32_t xr0[2], xr1[2];
+    xrows_of(q_c, 0, xr0);
+    xrows_of(q_c, 1, xr1);
+    static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 0, 0, xr0); });
+    static_for<16>([&](auto q) { dmaq(decltype(q)::value, ra_c, rb_c, 1, 1, xr1); });
+  }
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   static_for<16>([&](auto f) { read_frag(set0, f, K0{}, 0u); });
@@ -497,6 +546,8 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
       const bool here = t + 2 < nt;
       const Rsrc ra = here ? ra_c : ra_n, rb = here ? rb_c : rb_n;
       const int s2 = here ? t + 2 : t + 2 - nt;
+      uint32_t xr[2];
+      xrows_of(here ? q_c : q_n, s2, xr);
       // the shared slot plan (gemm_plan.h) with A = dY, B = X: dY's pieces of
       // step t+2 after barrier 1, X's after barrier 2, 13 before the wait
       constexpr int VMW = nt_plan_vmw();
@@ -511,7 +562,7 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
         static_for<16>([&](auto ec) {
           constexpr int E = decltype(ec)::value;
           if constexpr (kNtPlan.rd1[E] == S) read_frag(set1, std::integral_constant<int, E>{}, K1{}, so);
-          if constexpr (kNtPlan.dma[E] == S) dmaq(E, ra, rb, s2, slot);
+          if constexpr (kNtPlan.dma[E] == S) dmaq(E, ra, rb, s2, slot, xr);
           if constexpr (kNtPlan.rd0[E] == S) read_frag(set0, std::integral_constant<int, E>{}, K0{}, sn);
         });
         if constexpr (S == kNtPlan.b1 || S == kNtPlan.b2) {
@@ -532,39 +583,52 @@ wgrad4_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ 
     kstep(0, std::true_type{});
     for (int t = 1; t < nt; ++t) kstep(t, std::false_type{});
 
-    // epilogue: G[n][k .. k+3] (+)= acc, straight from registers
+    // epilogue: G[n][k .. k+3] (+)= acc, straight from registers (SPLIT: the
+    // item's fp32 block, ragged rows / columns included: the reduce skips them)
     fa::mfma_drain();
     int64_t n0, k0;
-    tile_org(i, n0, k0);
-    const int64_t kc = k0 + 128 * wk + 4 * (lane >> 4);
-    const int64_t nr = n0 + 128 * wn + (lane & 15);
+    int t0, blk;
+    tile_org(i, n0, k0, t0, blk);
+    if constexpr (SPLIT) {
+      float* wb = a.ws + (int64_t)blk * (TN * TK) + (128 * wn + (lane & 15)) * TK + 128 * wk +
+                  4 * (lane >> 4);
 #pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-      const int64_t n = nr + 16 * ii;
-      f32x4_* row = reinterpret_cast<f32x4_*>(g + n * K + kc);
-      if constexpr (ACCUM) {
-#pragma unroll
-        for (int jh = 0; jh < 8; jh += 4) {
-          f32x4_ o[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            o[j] = (n < N && kc + 16 * (jh + j) < K) ? __builtin_nontemporal_load(row + 4 * (jh + j))
-                                                      : f32x4_{0, 0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (n < N && kc + 16 * (jh + j) < K)
-              __builtin_nontemporal_store(o[j] + acc[ii][jh + j], row + 4 * (jh + j));
-        }
-      } else {
+      for (int ii = 0; ii < 8; ++ii)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (n < N && kc + 16 * j < K) __builtin_nontemporal_store(acc[ii][j], row + 4 * j);
+          __builtin_nontemporal_store(acc[ii][j], reinterpret_cast<f32x4_*>(wb + 16 * ii * TK + 16 * j));
+    } else {
+      const int64_t kc = k0 + 128 * wk + 4 * (lane >> 4);
+      const int64_t nr = n0 + 128 * wn + (lane & 15);
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii) {
+        const int64_t n = nr + 16 * ii;
+        f32x4_* row = reinterpret_cast<f32x4_*>(a.g + n * K + kc);
+        if constexpr (ACCUM) {
+#pragma unroll
+          for (int jh = 0; jh < 8; jh += 4) {
+            f32x4_ o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              o[j] = (n < N && kc + 16 * (jh + j) < K) ? __builtin_nontemporal_load(row + 4 * (jh + j))
+                                                        : f32x4_{0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (n < N && kc + 16 * (jh + j) < K)
+                __builtin_nontemporal_store(o[j] + acc[ii][jh + j], row + 4 * (jh + j));
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n < N && kc + 16 * j < K) __builtin_nontemporal_store(acc[ii][j], row + 4 * j);
+        }
       }
     }
     par ^= nt & 1;
     ra_c = ra_n;
     rb_c = rb_n;
-    make_rsrc(i + 2, ra_n, rb_n);
+    q_c = q_n;
+    make_rsrc(i + 2, ra_n, rb_n, q_n);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -682,8 +746,9 @@ int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K) {
 // wgrad_set_variant: A/B).  Round 4 measured the 4-wave kernel at 0.83-0.95x
 // (profiles/r4a_wgrad_variants.txt); with the vendor slot plan it shares with
 // gemm_nt6_k since round 5 it is 1.02-1.07x isolated and +1.6 % on the
-// headline step (profiles/r7r_wgrad_v4_ab.txt).  Token-mapped X (kept SP
-// gathers), M % 64 != 0 and > 2 GiB operands stay on wgrad_k.
+// headline step (profiles/r7r_wgrad_v4_ab.txt).  It also runs token-mapped X
+// (the kept SP gathers) and the split tails whose pieces are whole 64-token
+// steps; M % 64 != 0 and > 2 GiB operands stay on wgrad_k.
 int g_wvar = [] {
   const char* e = getenv("EMA_WGRAD_V");
   return (e && e[0] == '8') ? 8 : 4;
@@ -700,9 +765,10 @@ int num_cus() {
   return n;
 }
 
-bool wgrad4_ok(int64_t M, int64_t N, int64_t K) {
+// xrows: the physical X rows (a token map may reach past M)
+bool wgrad4_ok(int64_t M, int64_t N, int64_t K, int64_t xrows) {
   const int64_t lim = (int64_t)1 << 31;
-  return g_wvar == 4 && M % 64 == 0 && M >= 128 && M * N * 2 < lim && M * K * 2 < lim;
+  return g_wvar == 4 && M % 64 == 0 && M >= 128 && M * N * 2 < lim && xrows * K * 2 < lim;
 }
 
 // Tile grouping of the persistent kernel: groups of 8 n-tiles x all k-tiles on
@@ -717,12 +783,25 @@ int tile_group4() {
   return env != 0 ? env : 8;
 }
 
-template <typename T, bool ACCUM>
-void launch4(const void* dy, const void* x, float* g, int M, int N, int K, int tiles, int gn,
-             hipStream_t s) {
-  const int grid = tiles < num_cus() ? tiles : num_cus();
-  hipLaunchKernelGGL((wgrad4_k<T, ACCUM>), dim3(grid), dim3(256), 0, s, (const T*)dy, (const T*)x, g,
-                     M, N, K, gn, tiles);
+template <typename T, bool ACCUM, bool TM, bool SPLIT>
+void launch4(const W4Args& a, hipStream_t s) {
+  const int grid = a.nitems < num_cus() ? a.nitems : num_cus();
+  hipLaunchKernelGGL((wgrad4_k<T, ACCUM, TM, SPLIT>), dim3(grid), dim3(256), 0, s, a);
+}
+
+template <typename T>
+void launch4_dt(const W4Args& a, bool accumulate, bool split, hipStream_t s) {
+  const bool tm = a.xm.rows != 0;
+  if (split) {
+    if (tm) launch4<T, false, true, true>(a, s);
+    else launch4<T, false, false, true>(a, s);
+  } else if (accumulate) {
+    if (tm) launch4<T, true, true, false>(a, s);
+    else launch4<T, true, false, false>(a, s);
+  } else {
+    if (tm) launch4<T, false, true, false>(a, s);
+    else launch4<T, false, false, false>(a, s);
+  }
 }
 
 void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, int64_t K,
@@ -732,16 +811,23 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
   const bool split = pl.nsplit > 1 && ws != nullptr;
   const int main_tiles = split ? pl.main_tiles : pl.main_tiles + pl.tail_tiles;
   if (xm.rows != 0 && xm.rows % BM != 0) throw std::runtime_error("wgrad: token map groups must be 32-row multiples");
-  const bool v4 = main_tiles > 0 && xm.rows == 0 && wgrad4_ok(M, N, K);
+  // physical X rows the token map reaches (bindings.cpp checks them against x)
+  const int64_t xrows = xm.rows == 0 ? M
+                                     : (int64_t)(xm.n1 - 1) * xm.s1 +
+                                           (M / ((int64_t)xm.rows * xm.n1) - 1) * xm.s2 + xm.rows;
+  const bool v4 = wgrad4_ok(M, N, K, xrows);
+  // the split tail runs on the 4-wave kernel when its pieces are whole 64-token steps
+  // (EMA_WGRAD_TAIL4=0: the 8-wave kernel, for A/B)
+  static const bool tail4 = [] {
+    const char* e = getenv("EMA_WGRAD_TAIL4");
+    return !(e && e[0] == '0');
+  }();
+  const bool v4_tail = v4 && tail4 && split && M % (64 * pl.nsplit) == 0 && M / pl.nsplit >= 128;
   const int gn = v4 ? tile_group4() : tile_group((iN + TN - 1) / TN, (iK + TK - 1) / TK);
-  if (v4) {
-    if (dt == DT_BF16) {
-      if (accumulate) launch4<bf16, true>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
-      else launch4<bf16, false>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
-    } else if (dt == DT_F16) {
-      if (accumulate) launch4<fp16, true>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
-      else launch4<fp16, false>(dy, x, g, iM, iN, iK, main_tiles, gn, s);
-    }
+  W4Args a{dy, x, g, ws, iM, iN, iK, iM, gn, main_tiles, 0, main_tiles, (int)xrows, xm};
+  if (main_tiles > 0 && v4) {
+    if (dt == DT_BF16) launch4_dt<bf16>(a, accumulate, false, s);
+    else if (dt == DT_F16) launch4_dt<fp16>(a, accumulate, false, s);
   } else if (main_tiles > 0) {
     if (dt == DT_BF16) {
       if (accumulate) launch<bf16, true>(dy, x, g, iM, iN, iK, s, gn, 1, nullptr, 0, main_tiles, xm);
@@ -752,10 +838,18 @@ void wgrad_gemm(const void* dy, const void* x, float* g, int64_t M, int64_t N, i
     }
   }
   if (split) {
-    if (dt == DT_BF16)
+    if (v4_tail) {
+      a.msplit = iM / pl.nsplit;
+      a.nitems = pl.tail_tiles * pl.nsplit;
+      a.lin0 = pl.tail_lin0;
+      a.nlin = pl.tail_tiles;
+      if (dt == DT_BF16) launch4_dt<bf16>(a, false, true, s);
+      else if (dt == DT_F16) launch4_dt<fp16>(a, false, true, s);
+    } else if (dt == DT_BF16) {
       launch<bf16, false>(dy, x, g, iM, iN, iK, s, gn, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
-    else if (dt == DT_F16)
+    } else if (dt == DT_F16) {
       launch<fp16, false>(dy, x, g, iM, iN, iK, s, gn, pl.nsplit, ws, pl.tail_lin0, pl.tail_tiles, xm);
+    }
     hipLaunchKernelGGL(wgrad_split_reduce_k, dim3((unsigned)(pl.tail_tiles * 64)), dim3(256), 0, s,
                        ws, g, iN, iK, gn, pl.tail_lin0, pl.tail_tiles,
                        pl.nsplit, accumulate ? 1 : 0);

@@ -239,7 +239,7 @@ struct WgradPlan {
   int main_tiles, tail_lin0, tail_tiles, nsplit;
 };
 bool wgrad_supported(int64_t M, int64_t N, int64_t K);
-void wgrad_set_variant(int v);  // 8: 8-wave ping-pong (default), 4: persistent 4-wave kernel
+void wgrad_set_variant(int v);  // 4: persistent 4-wave kernel (default), 8: 8-wave ping-pong
 WgradPlan wgrad_plan(int64_t M, int64_t N, int64_t K);
 int64_t wgrad_workspace_floats(int64_t M, int64_t N, int64_t K);
 // Token (row) order of X relative to dY in a wgrad: logical token q of dY is

@@ -745,8 +745,10 @@ def test_wgrad_gemm_variants(variant, M, N, K):
 def test_wgrad_gemm_token_map(world, c, R, N, K):
     """x_map: X's rows are a two-level permutation of dY's tokens (the SP
     pipeline's piece-major gathers vs natural rows), read by the kernel
-    without a permutation copy; == the fp32 reference on the permuted X, and
-    bitwise equal to the kernel on an explicitly permuted copy."""
+    without a permutation copy; == the fp32 reference on the permuted X,
+    bitwise equal to the kernel on an explicitly permuted copy, and close to
+    the 8-wave kernel's token-map path (the 4-wave kernel runs the whole-tile
+    rounds and the split tails of these shapes)."""
     from epfl_megatron_amd.parallel.tensor.layers import _apply_token_map
     C = _ext()
     torch.manual_seed(4)
@@ -761,6 +763,13 @@ def test_wgrad_gemm_token_map(world, c, R, N, K):
         C.wgrad_gemm(dy, xp.contiguous(), g_ref, False)
         assert torch.equal(g, g_ref), xm
         _close(g, dy.float().t() @ xp.float(), atol=1e-3 * math.sqrt(M), msg=f"map {xm}")
+        C.wgrad_set_variant(8)  # the 8-wave kernel's token-map path on the same data
+        try:
+            g8 = torch.zeros(N, K, device=DEV)
+            C.wgrad_gemm(dy, x, g8, False, xm)
+        finally:
+            C.wgrad_set_variant(4)
+        _close(g8, g, atol=1e-3 * math.sqrt(M), msg=f"8-wave map {xm}")
     with pytest.raises(RuntimeError):
         C.wgrad_gemm(dy, x, torch.zeros(N, K, device=DEV), False, [R + 16, c, world * R, R])
 
