@@ -699,20 +699,25 @@ bool wgrad_supported(int64_t M, int64_t N, int64_t K) {
 // At least 2048 tokens per split, at most 4 x CUs pieces (workspace bound).
 // E.g. the 7B TP8 shards: qkv / fc2 (96 tiles) 2 ways (was 3: 288 pieces =
 // two rounds), fc1 (176 tiles) unsplit (was 2: 352 pieces, two rounds of
-// half tiles plus the partials' traffic).
+// half tiles plus the partials' traffic), dense (32 tiles) 8 ways.
 namespace {
 int best_split(int t, int64_t M, int ncu) {
   if (t <= 0) return 1;
   const double tile_us = 2.0 * TN * TK * (double)M / (1.3e15 / ncu) * 1e6;
   // per round: the pieces' compute + ~5 us of ring fill / epilogue
+  // a split must beat the whole tiles clearly (reduce launch, partial traffic);
+  // among the splits the cheapest wins.  Pieces of whole 64-token steps only
+  // (the 4-wave kernel's split form) when M allows them.
+  const double whole = ((t + ncu - 1) / ncu) * (tile_us + 5.0);
   int best = 1;
-  double best_c = ((t + ncu - 1) / ncu) * (tile_us + 5.0);
+  double best_c = whole * 0.95;
   for (int sp = 2; sp <= 16; ++sp) {
     if (M / sp < 2048 || t * sp > 4 * ncu) break;
+    if (M % 64 == 0 && M % (64 * sp) != 0) continue;
     const int rounds = (t * sp + ncu - 1) / ncu;
     const double c = rounds * (tile_us / sp + 5.0) +
                      (double)t * sp * TN * TK * 4.0 * 2.0 / 5e12 * 1e6 + 3.0;
-    if (c < best_c * 0.95) {  // a split must win clearly (reduce launch, partial traffic)
+    if (c < best_c) {
       best_c = c;
       best = sp;
     }

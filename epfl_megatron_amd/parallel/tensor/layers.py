@@ -415,7 +415,7 @@ def sp_allgather_gemm(x_local, w, glu_kind=None, keep=False):
         pre = torch.empty(world * rl, 2 * n, dtype=dt, device=dev)
         y = torch.empty(world * rl, n, dtype=dt, device=dev)
     if keep:
-        g = torch.empty((c, world * R, K), dtype=dt, device=dev)
+        g = _kept_buffer((c, world * R, K), dt, dev, group)
     else:
         g = get_global_memory_buffer().get_tensor((c, world * R, K), dt, "mpu")
     works = [comm.all_gather_into(g[j], x_local[j * R:(j + 1) * R], group=group, async_op=True)
@@ -429,6 +429,20 @@ def sp_allgather_gemm(x_local, w, glu_kind=None, keep=False):
             gemm_glu(g[j], w, glu_kind, pre, y, c_map=cmap)
     res = out if glu_kind is None else (pre, y)
     return (res, g) if keep else res
+
+
+# EMA_LOOPBACK_KEPT_POOL=0: fresh kept-gather tensors under the loopback too (A/B)
+_LOOP_KEPT_POOL = os.environ.get("EMA_LOOPBACK_KEPT_POOL", "1") != "0"
+
+
+def _kept_buffer(shape, dt, dev, group):
+    """Storage of an SP gather kept for the backward: a fresh tensor (the
+    caching allocator recycles it after the backward), or under the
+    simulated-TP loopback a pooled buffer whose simulated peers' slots are
+    written once (``GlobalMemoryBuffer.get_kept``)."""
+    if group is not None and _LOOP_KEPT_POOL and comm.loopback_size(group):
+        return get_global_memory_buffer().get_kept(shape, dt, dev)
+    return torch.empty(shape, dtype=dt, device=dev)
 
 
 def gathered_token_map(rl, world):
@@ -786,7 +800,7 @@ def _sp_mlp_forward(x_local, w1, w2, kind):
     # piece-major buffers: piece j's gathered rows at [world * off_j, world * (off_j + R_j));
     # kept for the fc1 wgrad (same piece order as every other MLP tensor)
     if sp_keep_gathered():
-        g = torch.empty(world * rl, H, dtype=dt, device=dev)
+        g = _kept_buffer((world * rl, H), dt, dev, group)
     else:
         g = get_global_memory_buffer().get_tensor((world * rl, H), dt, "mpu")
     gp = [g[world * o:world * (o + r)] for o, r in zip(offs, sizes)]

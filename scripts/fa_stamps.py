@@ -33,7 +33,11 @@ def run(C, b, s, nq, hd, causal):
         C.flash_attn_fwd(q, k, v, out, lse, b, s, s, nq, nq, hd, qs, ks, ks, os_, causal,
                          hd ** -0.5, None, None, None, None)
 
-    nblk = ((s + 255) // 256) * nq * b
+    # block rows: 32 per wave, 4 waves when the 8-wave grid is under 512
+    # blocks (csrc/flash_attn_fwd.hip flash_attn_waves)
+    blocks8 = ((s + 255) // 256) * nq * b
+    bm = 128 if blocks8 < 512 else 256
+    nblk = ((s + bm - 1) // bm) * nq * b
     buf = torch.zeros(nblk * 8 + 4096, dtype=torch.int64, device="cuda")
     for _ in range(3):
         call()
@@ -58,6 +62,13 @@ def run(C, b, s, nq, hd, causal):
         for a, bb in zip(rows, rows[1:]):
             gaps.append((bb[0] - a[3]) * 10e-3)
     busy = sum((r[3] - r[0]) for r in st) * 10e-3 / max(1, len(per_cu))
+    # causal balance: each CU's last end, and the query blocks it ran (mb =
+    # nmb - 1 - lin / (nq * b): heaviest first)
+    ends = sorted((max(r[3] for r in rows) - t0) * 10e-3 for rows in per_cu.values())
+    nmb = (s + bm - 1) // bm
+    idx = {id(r): i for i, r in enumerate(st)}
+    mbs = sorted((sorted(nmb - 1 - idx[id(r)] // (nq * b) for r in rows) for rows in per_cu.values()),
+                 key=lambda m: -sum(m))
     med = statistics.median
     rec = {"b": b, "s": s, "causal": causal, "blocks": nblk, "cus": len(per_cu),
            "span_us": round(span, 1), "busy_us_per_cu": round(busy, 1),
@@ -66,7 +77,11 @@ def run(C, b, s, nq, hd, causal):
            "gap_us_med": round(med(gaps), 2) if gaps else None,
            "gap_us_p90": round(sorted(gaps)[int(0.9 * len(gaps))], 2) if gaps else None,
            "blocks_per_cu_min_max": [min(nper), max(nper)],
-           "last_start_us": round((max(r[0] for r in st) - t0) * 10e-3, 1)}
+           "last_start_us": round((max(r[0] for r in st) - t0) * 10e-3, 1),
+           "nq": nq, "block_rows": bm,
+           "cu_end_us_min_med_max": [round(ends[0], 1), round(ends[len(ends) // 2], 1),
+                                     round(ends[-1], 1)],
+           "cu_qblocks_heaviest": mbs[:3], "cu_qblocks_lightest": mbs[-3:]}
     print(json.dumps(rec), flush=True)
     return rec
 
@@ -81,6 +96,8 @@ def main():
     for (b, s) in ((16, 1024), (4, 4096)):
         for causal in (False, True):
             res.append(run(C, b, s, 32, 128, causal))
+    # one TP rank of Llama-2-7B at TP = 8 (4 heads), the proxy's attention
+    res.append(run(C, 4, 4096, 4, 128, True))
     if args.json:
         json.dump(res, open(args.json, "w"), indent=1)
 

@@ -786,6 +786,9 @@ def test_wgrad_plan():
     # ragged 11 x 16 tiles: 2 x 176 pieces would take two rounds -> unsplit
     assert list(C.wgrad_plan(16384, 2752, 4096)) == [176, 176, 0, 1]
     assert list(C.wgrad_plan(16384, 1536, 4096)) == [0, 0, 96, 2]  # 2 x 96 in one round
+    # 7B TP8 dense shard: 8 pieces of whole 64-token steps (the 4-wave kernel's
+    # split form), not 7 (the cheapest split wins, not the first clear win)
+    assert list(C.wgrad_plan(16384, 4096, 512)) == [0, 0, 32, 8]
 
 
 def test_lt_gemm_layouts():

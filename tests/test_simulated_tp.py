@@ -43,6 +43,25 @@ def _sim_rank(rank, world, n):
     comm.all_gather_into(sc, x, group=g)
     out["ag_regen"] = bool(torch.isfinite(sc).all()) and all(
         torch.equal(sc[3 * i:3 * i + 3], x) for i in range(n))
+    # SP gathers kept for the backward come from a pool under the loopback: a
+    # buffer is handed out again only once nothing references it, and its
+    # peers' slots are written once per buffer
+    pool = get_global_memory_buffer()
+    k1 = pool.get_kept((3 * n, 2), torch.float32, "cpu")
+    k2 = pool.get_kept((3 * n, 2), torch.float32, "cpu")
+    busy = k1.data_ptr() != k2.data_ptr()
+    comm.all_gather_into(k1, x, group=g)
+    p1 = k1.data_ptr()
+    saved = k1[:3]  # a view (as autograd's saved tensor) keeps the buffer taken
+    del k1
+    k3 = pool.get_kept((3 * n, 2), torch.float32, "cpu")
+    busy = busy and k3.data_ptr() not in (p1, k2.data_ptr())
+    del saved, k3
+    k4 = pool.get_kept((3 * n, 2), torch.float32, "cpu")
+    comm.all_gather_into(k4, x + 100, group=g)
+    out["kept_pool"] = busy and k4.data_ptr() == p1 and torch.equal(k4[:3], x + 100) and all(
+        torch.equal(k4[3 * i:3 * i + 3], x) for i in range(1, n))
+    del k2, k4
     parts = torch.arange(n * 6, dtype=torch.float32).view(n * 3, 2)
     rs = torch.empty(3, 2)
     comm.reduce_scatter_into(rs, parts, group=g)
@@ -63,7 +82,7 @@ def _sim_rank(rank, world, n):
 def test_simulated_tp_rank_shapes_and_loopback():
     out = run_dist(_sim_rank, 1, 4)[0]
     assert out["tp"] == 4 and out["sp"]
-    assert out["ag"] and out["rs"] and out["ag_scratch"] and out["ag_regen"]
+    assert out["ag"] and out["rs"] and out["ag_scratch"] and out["ag_regen"] and out["kept_pool"]
     # h 64, 8 heads of 8 -> 2 heads per rank: qkv 3 * 2 * 8 = 48 rows; ffn 128 -> 2 * 32
     assert out["qkv"] == (48, 64) and out["fc1"] == (64, 64)
     assert out["loss"] == out["loss"] and out["loss"] > 0
