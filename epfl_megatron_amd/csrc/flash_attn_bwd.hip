@@ -475,7 +475,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nqb = (p.sq + BMW - 1) / BMW;
   const int nhb = p.nq * p.b;
-  const int lin = blockIdx.x;
+  int lin = blockIdx.x;
+  if (CAUSAL && p.pair_ncu > 0 && lin >= p.pair_ncu) lin = 3 * p.pair_ncu - 1 - lin;  // kernels.h
   const int qb = CAUSAL ? (nqb - 1 - lin / nhb) : lin / nhb;
   const int head = (lin % nhb) % p.nq, b = (lin % nhb) / p.nq;
   const int r = p.nq / p.nkv, g = head / r, hh = head - g * r;
@@ -710,7 +711,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
 }
 
 template <typename T, int HD>
-void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
+void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
+  AttnBwdParams P = P0;
   const AttnParams& p = P.f;
   // dK/dV: persistent, min(items, CUs) workgroups (EMA_FA_DKDV_GRID=full: one per item)
   static const int ncu = [] {
@@ -727,6 +729,8 @@ void launch_bwd(const AttnBwdParams& P, hipStream_t s) {
   const int wv = flash_attn_waves(p.b, p.sq, p.nq, HD);
   const dim3 gq(((p.sq + 255) / 256) * p.nq * p.b);
   const dim3 gq4(((p.sq + 127) / 128) * p.nq * p.b);
+  // dQ blocks in the forward's causal pairing; the dK/dV kernel reads none
+  P.f.pair_ncu = fa_pair_ncu(p.causal, wv == 4 ? gq4.x : gq.x, wv, HD);
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
     if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \

@@ -63,7 +63,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nmb = (p.sq + BMW - 1) / BMW;
   const int nhb = p.nq * p.b;
-  const int lin = blockIdx.x;
+  int lin = blockIdx.x;
+  if (CAUSAL && p.pair_ncu > 0 && lin >= p.pair_ncu) lin = 3 * p.pair_ncu - 1 - lin;
   const int mb = CAUSAL ? (nmb - 1 - lin / nhb) : lin / nhb;
   const int hb = lin % nhb;
   const int head = hb % p.nq, b = hb / p.nq;
@@ -347,9 +348,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
 
 
 template <typename T, int HD, int WAVES>
-void launch_fwd(const AttnParams& p, hipStream_t s) {
+void launch_fwd(const AttnParams& p0, hipStream_t s) {
   const int bmw = 32 * WAVES;
-  dim3 grid(((p.sq + bmw - 1) / bmw) * p.nq * p.b);
+  dim3 grid(((p0.sq + bmw - 1) / bmw) * p0.nq * p0.b);
+  AttnParams p = p0;
+  p.pair_ncu = fa_pair_ncu(p.causal, grid.x, WAVES, HD);
   if (p.causal)
     hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
   else
@@ -358,6 +361,32 @@ void launch_fwd(const AttnParams& p, hipStream_t s) {
 
 }  // namespace
 }  // namespace fa
+
+namespace {
+bool g_fa_pairing = [] {
+  const char* e = getenv("EMA_FA_PAIR");
+  return !(e && e[0] == '0');
+}();
+}  // namespace
+
+void fa_set_pairing(bool on) { g_fa_pairing = on; }
+
+// Causal balance of a fully resident grid (kernels.h AttnParams::pair_ncu).
+// Only the 4-wave head_dim-128 blocks run exactly two per CU (64 KiB of LDS
+// each); fa_stamps.py showed the pairs (k, k + ncu) on one CU: heavy-first
+// order alone gave the 7B TP8 rank (4 heads x 4 x 4096 tokens, 512 blocks)
+// CUs that ran query blocks 15 + 31 next to CUs that ran 0 + 16 (CU ends
+// 62-119 us).
+int fa_pair_ncu(int causal, long grid, int waves, int hd) {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+    return n;
+  }();
+  return (g_fa_pairing && causal && waves == 4 && hd == 128 && ncu > 0 && grid == 2L * ncu) ? ncu : 0;
+}
 
 bool flash_attn_supported(int hd, int dt) {
   return (hd == 64 || hd == 128) && (dt == DT_BF16 || dt == DT_F16);

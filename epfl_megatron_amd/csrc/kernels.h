@@ -142,7 +142,18 @@ struct AttnParams {
   // (default sk - sq, bottom-right aligned; a context-parallel pair whose keys
   // all precede its queries passes sk: no causal cut, document starts only)
   int coff;
+  // Set by the launchers (fa_pair_ncu): a causal forward / dQ grid of exactly
+  // two blocks per CU, all resident at once, dispatched one block per CU and
+  // then a second: blocks lin and lin + ncu share a CU, so the second round
+  // runs the query blocks lightest-first (block lin >= ncu takes the place of
+  // 3 ncu - 1 - lin in the heavy-first order) and every CU gets a heavy + a
+  // light block.  0: plain heavy-first order.
+  int pair_ncu;
 };
+// pair_ncu for a causal grid of `grid` blocks of `waves` waves (0: no pairing);
+// fa_set_pairing(false) turns it off (tests: bitwise equal outputs either way)
+int fa_pair_ncu(int causal, long grid, int waves, int hd);
+void fa_set_pairing(bool on);
 struct AttnBwdParams {
   AttnParams f;
   const void* dout;

@@ -395,6 +395,35 @@ def test_flash_attention_8wave(b, s, nq, nkv, causal):
     _attn_case(b, s, nq, nkv, 128, torch.bfloat16, causal, seed=s + nkv)
 
 
+def test_flash_attention_causal_pairing():
+    """A causal grid of exactly two 4-wave blocks per CU (one TP rank of a
+    TP-sharded model: 16 heads x 4096 tokens = 512 blocks of 128 rows) runs its
+    second round of query blocks lightest-first (kernels.h pair_ncu): == the
+    fp32 reference, and bitwise equal to the plain heavy-first order."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func
+    C = _ext()
+    b, s, nq, hd = 1, 4096, 16, 128
+    assert (s + 255) // 256 * nq * b < 512  # flash_attn_waves() picks 4
+    _attn_case(b, s, nq, nq, hd, torch.bfloat16, True, seed=17)
+    torch.manual_seed(18)
+    q, k, v = (torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    g = torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for on in (True, False):
+        C.fa_set_pairing(on)
+        try:
+            for t in (q, k, v):
+                t.grad = None
+            o = flash_attn_func(q, k, v, causal=True)
+            o.backward(g)
+            outs.append([o.detach().clone()] + [t.grad.clone() for t in (q, k, v)])
+        finally:
+            C.fa_set_pairing(True)
+    for a, bb, name in zip(outs[0], outs[1], ("o", "dq", "dk", "dv")):
+        assert torch.equal(a, bb), name
+
+
 def test_flash_attention_running_max_jump():
     """Online-softmax rescale branch forced: one key row aligned with one query
     row so that row's running max jumps by a large margin at a late tile
