@@ -42,7 +42,7 @@ from . import comm, state
 _LOCAL_KNOBS = ("EMA_TRACE", "EMA_STRICT_KERNELS", "EMA_OFFLOAD_ARCH", "EMA_EMBEDDED",
                 "EMA_XGMI_TIMEOUT_MS", "EMA_LOOPBACK_STREAM", "EMA_DGRAD_WT",
                 "EMA_NORM_MAIN_GRAD", "EMA_SKINNY_PACK", "EMA_SKINNY_WAVES",
-                "EMA_SKINNY_PERSIST", "EMA_WGRAD_MIN_TILES")
+                "EMA_SKINNY_PERSIST", "EMA_WGRAD_MIN_TILES", "EMA_LOOPBACK_KEPT_POOL")
 _LOCAL_PREFIXES = ("EMA_GEMM_", "EMA_WGRAD_", "EMA_FA_", "EMA_RMS_")
 
 
