@@ -98,6 +98,8 @@ def main():
             res.append(run(C, b, s, 32, 128, causal))
     # one TP rank of Llama-2-7B at TP = 8 (4 heads), the proxy's attention
     res.append(run(C, 4, 4096, 4, 128, True))
+    # Llama-2-70B at TP = 8 (8 heads per rank, micro-batch 1): one 4-wave block per CU
+    res.append(run(C, 1, 4096, 8, 128, True))
     if args.json:
         json.dump(res, open(args.json, "w"), indent=1)
 
