@@ -1275,6 +1275,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("docs"), py::arg("coff") = -1);
   m.def("fa_set_stamps", &fa_set_stamps);
   m.def("fa_set_pairing", &ema::fa_set_pairing);
+  m.def("fa_set_kv2", &ema::fa_set_kv2);
   m.def("greedy_tail", &greedy_tail);
   m.def("xgmi_create", &xgmi_create);
   m.def("xgmi_open", &xgmi_open);

@@ -44,22 +44,33 @@ namespace {
 typedef __attribute__((ext_vector_type(2))) float f2;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
-template <typename T, int HD, bool CAUSAL, int WAVES>
+// KV2 (WAVES = 8): the 128 query rows of a 4-wave block on 8 waves, waves
+// 4..7 repeating waves 0..3's rows over the second half of the block's key
+// tiles; each half keeps its own online softmax and 2-slot ring (every wave
+// loads pieces of both halves' tiles), and the halves' (m, l, O) merge through
+// LDS at the end.  For grids of at most one 4-wave block per CU (Llama-2-70B's
+// 8 heads per TP-8 rank: 256 causal blocks of 1..32 key tiles), where the
+// heaviest block sets the kernel time and one wave per SIMD hides no latency.
+template <typename T, int HD, bool CAUSAL, int WAVES, bool KV2 = false>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnParams p) {
   typedef typename MT<T>::x8 x8;
   typedef typename MT<T>::x4 x4;
-  constexpr int BMW = WAVES * 32, KT = 64;
+  static_assert(!KV2 || WAVES == 8, "KV2: two 4-wave halves");
+  constexpr int RW = KV2 ? 4 : WAVES;  // waves holding distinct query rows
+  constexpr int BMW = RW * 32, KT = 64;
   constexpr int KS = HD / 16, DT = HD / 32;
   constexpr int ROWB = HD * 2, RG = 8 * ROWB, PIECES = KT * ROWB / 1024, PPW = PIECES / WAVES;
   constexpr int TB = KT * ROWB;  // bytes of one K (or V) tile
-  constexpr int NB = WAVES == 8 ? 3 : 2;
+  constexpr int NB = (WAVES == 8 && !KV2) ? 3 : 2;
+  constexpr int NG = KV2 ? 2 : 1;  // key halves, each with its own ring
   static_assert(PIECES % WAVES == 0, "pieces per wave");
-  __shared__ __attribute__((aligned(1024))) char lds[NB * 2 * TB];
+  __shared__ __attribute__((aligned(1024))) char lds[NG * NB * 2 * TB];
 
   const int tid = threadIdx.x;
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if (p.stamps) st0 = fa::wall_stamp();
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int grp = KV2 ? (wave >> 2) : 0, rw = KV2 ? (wave & 3) : wave;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nmb = (p.sq + BMW - 1) / BMW;
   const int nhb = p.nq * p.b;
@@ -75,7 +86,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   const T* K = (const T*)p.k + (int64_t)b * p.k_sb + (int64_t)g * p.k_sg;
   const T* V = (const T*)p.v + (int64_t)b * p.v_sb + (int64_t)g * p.v_sg;
 
-  const int m0 = mb * BMW + wave * 32;
+  const int m0 = mb * BMW + rw * 32;
   const int qrow = m0 + c;
   const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;
 
@@ -112,8 +123,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     srow[i] = 8 * (o / RG) + rem2 / 64;
     schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
   }
-  auto prefetch = [&](int t, int slot) {
-    char* kl = lds + slot * 2 * TB;
+  auto prefetch = [&](int t, int slot, int g) {
+    char* kl = lds + (g * NB + slot) * 2 * TB;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int pc = wave * PPW + i;
@@ -127,8 +138,19 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
                                        16, 0, 0);
     }
   };
-  if (t0 < ntiles) prefetch(t0, t0 % NB);
-  if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB);
+  // this wave's key tiles [gs, ge) over niter barrier-synchronous iterations
+  // (KV2: the halves [t0, t0 + half) and [t0 + half, ntiles))
+  const int ntot = ntiles > t0 ? ntiles - t0 : 0;
+  const int half = KV2 ? (ntot + 1) / 2 : ntot;
+  const int niter = half;
+  const int gs = t0 + (grp ? half : 0), ge = KV2 && grp == 0 ? t0 + half : ntiles;
+  if constexpr (KV2) {
+    if (half > 0) prefetch(t0, 0, 0);
+    if (t0 + half < ntiles) prefetch(t0 + half, 0, 1);
+  } else {
+    if (t0 < ntiles) prefetch(t0, t0 % NB, 0);
+    if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB, 0);
+  }
 
   x8 qf[KS];
 #pragma unroll
@@ -137,7 +159,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     const float *rc, *rs;
     rope_rows<HD>(p, b, qrow_c, rc, rs);
     rope_rows_fwd<T, KS>(qf, rc, rs, h);  // table loads batched (not one round trip per fragment)
-    if (qrow < p.sq) {
+    // (KV2: written back after the merge -- the other half reads these rows now)
+    if (!KV2 && qrow < p.sq) {
       T* Qw = const_cast<T*>(Q) + (int64_t)qrow * p.q_ss + 8 * h;
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) *reinterpret_cast<x8*>(Qw + kk * 16) = qf[kk];
@@ -162,13 +185,21 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
   __syncthreads();  // vmcnt(0) + barrier: tile 0 (and 1) landed
   if (p.stamps) st1 = fa::wall_stamp();
 
-  for (int t = t0; t < ntiles; ++t) {
+  for (int it = 0; it < niter; ++it) {
+    const int t = gs + it;
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
     // retired before the barrier that ended tile t-1
-    if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
-    if (t < wtiles && t >= wt0) {
+    if constexpr (KV2) {
+      if (it + 1 < niter) {
+        prefetch(t0 + it + 1, (it + 1) & 1, 0);
+        if (t0 + half + it + 1 < ntiles) prefetch(t0 + half + it + 1, (it + 1) & 1, 1);
+      }
+    } else {
+      if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB, 0);
+    }
+    if (t < ge && t < wtiles && t >= wt0) {
       const int n0 = t * KT;
-      const char* kl = lds + (t % NB) * 2 * TB;
+      const char* kl = lds + (KV2 ? grp * NB + (it & 1) : t % NB) * 2 * TB;
       const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
       const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
       f32x16 s0, s1;
@@ -286,8 +317,41 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
     }
   }
 
+  if constexpr (KV2) {
+    // merge the second half's (m, l, O) into the first's (the loop ended on a
+    // barrier: the rings are drained); lane-contiguous floats, conflict-free
+    float* ml = reinterpret_cast<float*>(lds);
+    float* ob = ml + 4 * 2 * 64;
+    if (grp == 1) {
+      ml[(rw * 2) * 64 + lane] = m_i;
+      ml[(rw * 2 + 1) * 64 + lane] = l_i;
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ob[((rw * DT + d) * 16 + i) * 64 + lane] = o[d][i];
+    }
+    __syncthreads();
+    if (grp == 0) {
+      const float mB = ml[(rw * 2) * 64 + lane], lB = ml[(rw * 2 + 1) * 64 + lane];
+      const float m = fmaxf(m_i, mB);
+      if (m != -INFINITY) {
+        const float aA = __builtin_amdgcn_exp2f(m_i - m), aB = __builtin_amdgcn_exp2f(mB - m);
+        l_i = l_i * aA + lB * aB;
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[d][i] = o[d][i] * aA + ob[((rw * DT + d) * 16 + i) * 64 + lane] * aB;
+        m_i = m;
+      }
+      if (p.rope_cos && qrow < p.sq) {
+        T* Qw = const_cast<T*>(Q) + (int64_t)qrow * p.q_ss + 8 * h;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) *reinterpret_cast<x8*>(Qw + kk * 16) = qf[kk];
+      }
+    }
+  }
   if (p.stamps) st2 = fa::wall_stamp();
-  if (qrow < p.sq) {
+  if ((!KV2 || grp == 0) && qrow < p.sq) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
     const float lse_j = l_i > 0.f ? (m_i + __log2f(l_i)) * 0.6931471805599453f : -INFINITY;
     float* lp = p.lse + (int64_t)b * p.lse_sb + (int64_t)head * p.lse_sh + qrow;
@@ -347,29 +411,41 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_fwd_k(const AttnPara
 }
 
 
-template <typename T, int HD, int WAVES>
+template <typename T, int HD, int WAVES, bool KV2 = false>
 void launch_fwd(const AttnParams& p0, hipStream_t s) {
-  const int bmw = 32 * WAVES;
+  const int bmw = 32 * (KV2 ? 4 : WAVES);
   dim3 grid(((p0.sq + bmw - 1) / bmw) * p0.nq * p0.b);
   AttnParams p = p0;
-  p.pair_ncu = fa_pair_ncu(p.causal, grid.x, WAVES, HD);
+  p.pair_ncu = KV2 ? 0 : fa_pair_ncu(p.causal, grid.x, WAVES, HD);
   if (p.causal)
-    hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, true, WAVES, KV2>), grid, dim3(64 * WAVES), 0, s, p);
   else
-    hipLaunchKernelGGL((fa_fwd_k<T, HD, false, WAVES>), grid, dim3(64 * WAVES), 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_k<T, HD, false, WAVES, KV2>), grid, dim3(64 * WAVES), 0, s, p);
 }
 
 }  // namespace
 }  // namespace fa
 
 namespace {
-bool g_fa_pairing = [] {
-  const char* e = getenv("EMA_FA_PAIR");
+// an environment default read on first use (function-local static), which a
+// setter overrides (tests / A/B in one process)
+bool env_on(const char* name) {
+  const char* e = getenv(name);
   return !(e && e[0] == '0');
-}();
+}
+int g_fa_pairing_set = -1;  // -1: EMA_FA_PAIR
+int g_fa_kv2_set = -1;      // -1: EMA_FA_KV2
+bool fa_pairing_on() {
+  static const bool env = env_on("EMA_FA_PAIR");
+  return g_fa_pairing_set >= 0 ? g_fa_pairing_set != 0 : env;
+}
+bool fa_kv2_on() {
+  static const bool env = env_on("EMA_FA_KV2");
+  return g_fa_kv2_set >= 0 ? g_fa_kv2_set != 0 : env;
+}
 }  // namespace
 
-void fa_set_pairing(bool on) { g_fa_pairing = on; }
+void fa_set_pairing(bool on) { g_fa_pairing_set = on ? 1 : 0; }
 
 // Causal balance of a fully resident grid (kernels.h AttnParams::pair_ncu).
 // Only the 4-wave head_dim-128 blocks run exactly two per CU (64 KiB of LDS
@@ -377,7 +453,7 @@ void fa_set_pairing(bool on) { g_fa_pairing = on; }
 // order alone gave the 7B TP8 rank (4 heads x 4 x 4096 tokens, 512 blocks)
 // CUs that ran query blocks 15 + 31 next to CUs that ran 0 + 16 (CU ends
 // 62-119 us).
-int fa_pair_ncu(int causal, long grid, int waves, int hd) {
+static int fa_ncu() {
   static const int ncu = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -385,7 +461,12 @@ int fa_pair_ncu(int causal, long grid, int waves, int hd) {
       n = 0;
     return n;
   }();
-  return (g_fa_pairing && causal && waves == 4 && hd == 128 && ncu > 0 && grid == 2L * ncu) ? ncu : 0;
+  return ncu;
+}
+
+int fa_pair_ncu(int causal, long grid, int waves, int hd) {
+  const int ncu = fa_ncu();
+  return (fa_pairing_on() && causal && waves == 4 && hd == 128 && ncu > 0 && grid == 2L * ncu) ? ncu : 0;
 }
 
 bool flash_attn_supported(int hd, int dt) {
@@ -402,7 +483,22 @@ int flash_attn_waves(int b, int sq, int nq, int hd) {
   return (hd == 64 || blocks8 < 512) ? 4 : 8;
 }
 
+void fa_set_kv2(bool on) { g_fa_kv2_set = on ? 1 : 0; }
+
+// The split-key forward (fa_fwd_k KV2) for head_dim-128 grids of at most one
+// 4-wave block per CU
+static bool fa_use_kv2(int b, int sq, int nq, int hd) {
+  const long blocks4 = (long)((sq + 127) / 128) * nq * b;
+  const int ncu = fa_ncu();
+  return fa_kv2_on() && hd == 128 && ncu > 0 && blocks4 <= ncu;
+}
+
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
+  if (fa_use_kv2(p.b, p.sq, p.nq, p.hd)) {
+    if (dt == DT_BF16) fa::launch_fwd<bf16, 128, 8, true>(p, s);
+    else fa::launch_fwd<fp16, 128, 8, true>(p, s);
+    return;
+  }
   const bool w4 = flash_attn_waves(p.b, p.sq, p.nq, p.hd) == 4;
   if (dt == DT_BF16) {
     if (p.hd == 128) w4 ? fa::launch_fwd<bf16, 128, 4>(p, s) : fa::launch_fwd<bf16, 128, 8>(p, s);

@@ -154,6 +154,9 @@ struct AttnParams {
 // fa_set_pairing(false) turns it off (tests: bitwise equal outputs either way)
 int fa_pair_ncu(int causal, long grid, int waves, int hd);
 void fa_set_pairing(bool on);
+// the split-key forward for grids of at most one 4-wave block per CU (on by
+// default; EMA_FA_KV2=0 / fa_set_kv2(false): the 4-wave forward)
+void fa_set_kv2(bool on);
 struct AttnBwdParams {
   AttnParams f;
   const void* dout;

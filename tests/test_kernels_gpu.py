@@ -424,6 +424,33 @@ def test_flash_attention_causal_pairing():
         assert torch.equal(a, bb), name
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_split_key_forward(causal):
+    """One TP rank of Llama-2-70B at TP = 8 (8 query heads on one KV head, 4096
+    tokens: 256 blocks of 128 rows, one per CU) runs the split-key forward
+    (fa_fwd_k KV2: two 4-wave halves of the key range, merged through LDS);
+    == the fp32 reference with it on and off, and the two close to each other.
+    Smaller head_dim-128 grids in this file run it too."""
+    from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
+    C = _ext()
+    b, s, nq, nkv, hd = 1, 4096, 8, 1, 128
+    _attn_case(b, s, nq, nkv, hd, torch.bfloat16, causal, seed=21)
+    torch.manual_seed(22)
+    q = torch.randn(b, s, nq, hd, device=DEV, dtype=torch.bfloat16)
+    k, v = (torch.randn(b, s, nkv, hd, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    ref = attention_ref(q.float(), k.float(), v.float(), causal=causal)
+    outs = []
+    for on in (True, False):
+        C.fa_set_kv2(on)
+        try:
+            outs.append(flash_attn_func(q, k, v, causal=causal))
+        finally:
+            C.fa_set_kv2(True)
+    _close(outs[0], ref, 2e-2, 2e-2, "split-key forward")
+    _close(outs[1], ref, 2e-2, 2e-2, "4-wave forward")
+    _close(outs[0], outs[1], 2e-2, 2e-2, "split-key vs 4-wave")
+
+
 def test_flash_attention_running_max_jump():
     """Online-softmax rescale branch forced: one key row aligned with one query
     row so that row's running max jumps by a large margin at a late tile
