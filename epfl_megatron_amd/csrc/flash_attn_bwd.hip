@@ -458,20 +458,28 @@ __global__ __launch_bounds__(256) void fa_dkv_reduce_k(const AttnBwdParams P) {
 // MFMAs, written to the other buffer after them), flat grid with the query
 // blocks holding the most keys (causal) dispatched first.  Same math as
 // fa_bwd_dq_k.
-template <typename T, int HD, bool CAUSAL, int WAVES>
+// KV2 (WAVES = 8): the split-key form of the forward's fa_fwd_k KV2 -- the 128
+// rows of a 4-wave block on 8 waves, waves 4..7 over the second half of the
+// key tiles; their dQ partials are added through LDS at the end.
+template <typename T, int HD, bool CAUSAL, int WAVES, bool KV2 = false>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const AttnBwdParams P) {
   typedef typename MT<T>::x8 x8;
   typedef typename MT<T>::x4 x4;
   const AttnParams& p = P.f;
-  constexpr int NT = WAVES * 64, BMW = WAVES * 32;
+  static_assert(!KV2 || WAVES == 8, "KV2: two 4-wave halves");
+  constexpr int RW = KV2 ? 4 : WAVES;  // waves holding distinct query rows
+  constexpr int NT = WAVES * 64, BMW = RW * 32;
   constexpr int KS = HD / 16, DT = HD / 32, CPR = HD / 8;
   // K/V ring depth: 3 tiles (two in flight behind the one being read) for the
   // one-block-per-CU 8-wave form; 2 for the 4-wave form (two blocks per CU)
-  constexpr int NB = WAVES == 8 ? DQ_RING : 2;
-  __shared__ __attribute__((aligned(16))) T lds[NB * 2 * KT * HD];
+  // and for each half of the split-key form
+  constexpr int NB = (WAVES == 8 && !KV2) ? DQ_RING : 2;
+  constexpr int NG = KV2 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) T lds[NG * NB * 2 * KT * HD];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int grp = KV2 ? (wave >> 2) : 0, rw = KV2 ? (wave & 3) : wave;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nqb = (p.sq + BMW - 1) / BMW;
   const int nhb = p.nq * p.b;
@@ -481,7 +489,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   const int head = (lin % nhb) % p.nq, b = (lin % nhb) / p.nq;
   const int r = p.nq / p.nkv, g = head / r, hh = head - g * r;
   const int off = p.coff;
-  const int q0w = qb * BMW + wave * 32;
+  const int q0w = qb * BMW + rw * 32;
   const int qrow = q0w + c;
   const int qrow_c = qrow < p.sq ? qrow : p.sq - 1;
   const float sl2 = p.scale * 1.4426950408889634f;
@@ -529,8 +537,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
     srow[i] = 8 * (o / RG) + rem2 / 64;
     schunk[i] = 4 * (rem / 512) + (((rem2 % 64) / 16) ^ ((srow[i] >> 2) & 3));
   }
-  auto prefetch = [&](int t, int buf) {
-    char* kl = reinterpret_cast<char*>(lds + buf * 2 * KT * HD);
+  auto prefetch = [&](int t, int buf, int g) {
+    char* kl = reinterpret_cast<char*>(lds + (g * NB + buf) * 2 * KT * HD);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int pc = wave * PPW + i;
@@ -545,8 +553,18 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
           (__attribute__((address_space(3))) void*)(kl + KT * ROWB + pc * 1024), 16, 0, 0);
     }
   };
-  if (t0 < ntiles) prefetch(t0, t0 % NB);
-  if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB);
+  // this wave's key tiles [gs, ge) over niter barrier-synchronous iterations
+  const int ntot = ntiles > t0 ? ntiles - t0 : 0;
+  const int half = KV2 ? (ntot + 1) / 2 : ntot;
+  const int niter = half;
+  const int gs = t0 + (grp ? half : 0), ge = KV2 && grp == 0 ? t0 + half : ntiles;
+  if constexpr (KV2) {
+    if (half > 0) prefetch(t0, 0, 0);
+    if (t0 + half < ntiles) prefetch(t0 + half, 0, 1);
+  } else {
+    if (t0 < ntiles) prefetch(t0, t0 % NB, 0);
+    if (NB == 3 && t0 + 1 < ntiles) prefetch(t0 + 1, (t0 + 1) % NB, 0);
+  }
 
   x8 qf[KS], df[KS];
 #pragma unroll
@@ -569,7 +587,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
       for (int e = 0; e < 8; ++e) dlt += (float)ov[e] * (float)df[kk][e];
     }
     dlt += __shfl_xor(dlt, 32, 64);
-    if (h == 0 && qrow < p.sq) {
+    if (h == 0 && qrow < p.sq && grp == 0) {
       P.ndelta[rb + qrow] = -dlt;
       P.lse2[rb + qrow] = lse2;
     }
@@ -590,16 +608,24 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   }
   __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
 
-  for (int t = t0; t < ntiles; ++t) {
-    const int buf = t % NB;
+  for (int it = 0; it < niter; ++it) {
+    const int t = gs + it;
+    const int buf = KV2 ? grp * NB + (it & 1) : t % NB;
     // WAR: tile t+NB-1 overwrites the slot of tile t-1, whose reads every wave
     // retired before the barrier that ended tile t-1
-    if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB);
+    if constexpr (KV2) {
+      if (it + 1 < niter) {
+        prefetch(t0 + it + 1, (it + 1) & 1, 0);
+        if (t0 + half + it + 1 < ntiles) prefetch(t0 + half + it + 1, (it + 1) & 1, 1);
+      }
+    } else {
+      if (t + NB - 1 < ntiles) prefetch(t + NB - 1, (t + NB - 1) % NB, 0);
+    }
     const char* kl = reinterpret_cast<const char*>(lds + buf * 2 * KT * HD);
     const char* vl = kl + KT * ROWB;
     const uint32_t trv0 = (uint32_t)(uintptr_t)(kl + trb[0]);
     const uint32_t trv1 = (uint32_t)(uintptr_t)(kl + trb[1]);
-    if (t < wtiles && t >= wt0) {
+    if (t < ge && t < wtiles && t >= wt0) {
       static_for<KT / 32>([&](auto subc) {
         constexpr int sub = decltype(subc)::value;
         const int kb = t * KT + sub * 32;
@@ -684,7 +710,25 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void fa_bwd_dq2_k(const Attn
   }
 
   mfma_drain();
-  if (qrow < p.sq) {
+  if constexpr (KV2) {
+    // add the second half's dQ partials (the loop ended on a barrier: the rings
+    // are drained); lane-contiguous floats, conflict-free
+    float* ob = reinterpret_cast<float*>(lds);
+    if (grp == 1) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ob[((rw * DT + d) * 16 + i) * 64 + lane] = dq[d][i];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dq[d][i] += ob[((rw * DT + d) * 16 + i) * 64 + lane];
+    }
+  }
+  if ((!KV2 || grp == 0) && qrow < p.sq) {
     T* DQ = (T*)P.dq + (int64_t)b * p.q_sb + (int64_t)qrow * p.q_ss + (int64_t)g * p.q_sg +
             (int64_t)hh * p.q_sh;
     const float *rc = nullptr, *rs = nullptr;
@@ -730,10 +774,13 @@ void launch_bwd(const AttnBwdParams& P0, hipStream_t s) {
   const dim3 gq(((p.sq + 255) / 256) * p.nq * p.b);
   const dim3 gq4(((p.sq + 127) / 128) * p.nq * p.b);
   // dQ blocks in the forward's causal pairing; the dK/dV kernel reads none
-  P.f.pair_ncu = fa_pair_ncu(p.causal, wv == 4 ? gq4.x : gq.x, wv, HD);
+  // the split-key dQ on the grids the forward runs split-key
+  const bool kv2 = HD == 128 && flash_attn_kv2(p.b, p.sq, p.nq, HD);
+  P.f.pair_ncu = kv2 ? 0 : fa_pair_ncu(p.causal, wv == 4 ? gq4.x : gq.x, wv, HD);
 #define EMA_FA_BWD(C)                                                                     \
   {                                                                                       \
-    if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \
+    if (kv2) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8, true>), gq4, dim3(512), 0, s, P); \
+    else if (wv == 4) hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 4>), gq4, dim3(256), 0, s, P); \
     else hipLaunchKernelGGL((fa_bwd_dq2_k<T, HD, C, 8>), gq, dim3(512), 0, s, P);         \
     hipLaunchKernelGGL((fa_bwd_dkdv2_k<T, HD, C>), gkv, dim3(256), 0, s, P);              \
     if (P.kv_split > 1)                                                                   \

@@ -485,16 +485,16 @@ int flash_attn_waves(int b, int sq, int nq, int hd) {
 
 void fa_set_kv2(bool on) { g_fa_kv2_set = on ? 1 : 0; }
 
-// The split-key forward (fa_fwd_k KV2) for head_dim-128 grids of at most one
-// 4-wave block per CU
-static bool fa_use_kv2(int b, int sq, int nq, int hd) {
+// The split-key forward and dQ (fa_fwd_k / fa_bwd_dq2_k KV2) for head_dim-128
+// grids of at most one 4-wave block per CU
+bool flash_attn_kv2(int b, int sq, int nq, int hd) {
   const long blocks4 = (long)((sq + 127) / 128) * nq * b;
   const int ncu = fa_ncu();
   return fa_kv2_on() && hd == 128 && ncu > 0 && blocks4 <= ncu;
 }
 
 void flash_attn_fwd(const AttnParams& p, int dt, hipStream_t s) {
-  if (fa_use_kv2(p.b, p.sq, p.nq, p.hd)) {
+  if (flash_attn_kv2(p.b, p.sq, p.nq, p.hd)) {
     if (dt == DT_BF16) fa::launch_fwd<bf16, 128, 8, true>(p, s);
     else fa::launch_fwd<fp16, 128, 8, true>(p, s);
     return;

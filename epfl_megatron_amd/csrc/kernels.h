@@ -157,6 +157,7 @@ void fa_set_pairing(bool on);
 // the split-key forward for grids of at most one 4-wave block per CU (on by
 // default; EMA_FA_KV2=0 / fa_set_kv2(false): the 4-wave forward)
 void fa_set_kv2(bool on);
+bool flash_attn_kv2(int b, int sq, int nq, int hd);  // that grid runs split-key
 struct AttnBwdParams {
   AttnParams f;
   const void* dout;

@@ -428,8 +428,9 @@ def test_flash_attention_causal_pairing():
 def test_flash_attention_split_key_forward(causal):
     """One TP rank of Llama-2-70B at TP = 8 (8 query heads on one KV head, 4096
     tokens: 256 blocks of 128 rows, one per CU) runs the split-key forward
-    (fa_fwd_k KV2: two 4-wave halves of the key range, merged through LDS);
-    == the fp32 reference with it on and off, and the two close to each other.
+    (fa_fwd_k KV2: two 4-wave halves of the key range, merged through LDS) and
+    the split-key dQ (fa_bwd_dq2_k KV2, partials added through LDS): fwd + bwd
+    == the fp32 reference; the forward with it on and off close to each other.
     Smaller head_dim-128 grids in this file run it too."""
     from epfl_megatron_amd.ops.attention import flash_attn_func, attention_ref
     C = _ext()
